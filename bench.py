@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""bench.py — Mray/s and ms/frame of the MI355X ray tracer on BASELINE.json's workload.
+
+Workload (N=1): configs[1] of BASELINE.json = c2: 1920x1080, 8 spheres + checkerboard, 1 light,
+1 reflection bounce (SURVEY.md Appendix B scene, canonical framing pitch = 500/W).  One step = one full
+frame traced by rt_render_kernel (one launch) writing the RGBA32F framebuffer (unclamped HDR, the
+parity image) and the RGBA8 display image, all buffers resident in HBM.  Rays are the reference's
+actually-traced count (primary + reflected + shadow), taken from the kernel's own
+per-pixel ray counters before the timed region and checked against the reference's pinned total.
+
+N>1 (torch.distributed.run, one rank per GPU, RCCL): weak scaling by default — a step is N frames, every
+frame row-banded over all N ranks (band height 8, round-robin), each rank's slabs of all N frames
+gathered to rank 0 over RCCL in one collective, and rank 0 puts every frame back into image order with
+rt_unshuffle_dev.  Per-GPU work stays one frame.  `--scaling strong` renders ONE frame per step split
+over the N ranks (the c4 design).
+
+Printed: ONE JSON line on rank 0 (contract in the task statement) with `roofline` (HBM-write roofline of
+the dominant kernel, per north_star) and `roofline_fp64` (its FP64 VALU roofline) and `cpu_baseline`
+(the bit-exact C restatement, oracle/rt_oracle.c, timed on this host's cores, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mray/s (primary+shadow+reflect) and ms/frame at 1920×1080"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s spec)
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector spec (an FMA counts 2)
+# Algorithmic FP64 operations per frame (add, mul, div, sqrt = 1 each; SURVEY.md §8d counting restatement)
+FP64_FLOPS_PER_FRAME = {"c1": 71.4e6, "c2": 1.038e9, "c3": 5.417e9, "c4": 5.417e9, "c5": 122.6e9}
+BYTES_PER_PIXEL = 16 + 4       # RGBA32F framebuffer + RGBA8 display image written per pixel
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c5"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--band-height", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--profile-kernel-only", action="store_true",
+                    help="skip parity/ray-count/cpu legs (for rocprofv3 runs)")
+    return ap.parse_args()
+
+
+def cpu_threads() -> int:
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:
+        return max(1, min(16, os.cpu_count() or 1))
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main() -> int:
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from ray_tracer_fragment_shader_amd import scenes
+    from ray_tracer_fragment_shader_amd.distributed import BandPlan, assemble_on_device, gather_slabs
+    from ray_tracer_fragment_shader_amd.tracer import Tracer
+
+    if not torch.cuda.is_available():
+        print("bench.py needs a HIP GPU", file=sys.stderr)
+        return 2
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    cfg = scenes.CONFIGS[args.config]
+    W, H, B = cfg.width, cfg.height, cfg.depth
+    scene = cfg.scene()
+    cam = cfg.camera()
+    tr = Tracer(local)
+    tr.set_scene(scene)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+
+    frames = world if (world > 1 and args.scaling == "weak") else 1
+    plan = BandPlan(H, world, args.band_height)
+    rows = plan.rows(rank) if world > 1 else None
+    nl = plan.local[rank]
+    slab = plan.slab_rows
+    out32 = torch.empty((frames, slab, W, 4), dtype=torch.float32, device=dev)
+    out8 = torch.empty((frames, slab, W, 4), dtype=torch.uint8, device=dev)
+    image8 = torch.empty((frames, H, W, 4), dtype=torch.uint8, device=dev) if (rank == 0 and world > 1) else None
+
+    # ---- parity + ray count (outside the timed region) ----------------------------------------------
+    parity = "skipped"
+    rays_frame = scenes.PINNED_RAYS.get(args.config)
+    if not args.profile_kernel_only:
+        chk = tr.render(cam, W, H, B, rgba32f=False, rgb64f=True, raycount=True)
+        torch.cuda.synchronize()
+        rc = chk["raycount"].cpu().numpy().view(np.uint32)
+        rays_frame = int((rc & 0xFFFF).sum()) + int((rc >> 16).sum())
+        pinned = scenes.PINNED_RAYS.get(args.config)
+        if pinned is not None and rays_frame != pinned:
+            raise SystemExit(f"ray count {rays_frame} != reference {pinned}")
+        g = np.load(os.path.join(ROOT, "tests", "golden", f"frames_{args.config}.npz"))
+        got = chk["rgb64f"].cpu().numpy()[g["pj"], g["pi"]]
+        if not np.array_equal(got, g["samples"]):
+            raise SystemExit(f"parity failure: max err {np.abs(got - g['samples']).max()}")
+        parity = "bit-exact on 4096 sampled pixels vs the reference's rayTraceRay (tests/golden)"
+        del chk, rc
+
+    def step(evs=None):
+        for f in range(frames):
+            if evs is not None:
+                evs[0].append(torch.cuda.Event(enable_timing=True))
+                evs[0][-1].record(stream)
+            tr.render_into(cam, W, H, B, {"rgba32f": out32[f], "rgba8": out8[f]}, rows=rows, stream=stream)
+            if evs is not None:
+                evs[1].append(torch.cuda.Event(enable_timing=True))
+                evs[1][-1].record(stream)
+        if world > 1:
+            gathered = gather_slabs(out8, world)
+            if rank == 0:
+                allr = torch.stack(gathered)                 # [world, frames, slab, W, 4]
+                for f in range(frames):
+                    assemble_on_device(allr[:, f].contiguous(), plan, W, image8[f], stream)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    evs = ([], [])
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(evs)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in zip(*evs)]
+    avg_kern_ms = sum(kern_ms) / len(kern_ms)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    rays_step = rays_frame * frames
+    value = rays_step * args.steps / elapsed / 1e6
+    ms_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        bytes_launch = nl * W * BYTES_PER_PIXEL
+        achieved = bytes_launch / (avg_kern_ms * 1e-3) / 1e9
+        flops_launch = FP64_FLOPS_PER_FRAME[args.config] * nl / H
+        tflops = flops_launch / (avg_kern_ms * 1e-3) / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+        if os.path.exists(pmc) and world == 1:
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        res = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "ms_per_frame": round(ms_step / frames, 4),
+            "higher_is_better": True,
+            "scaling": args.scaling if world > 1 else "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: canonical scene of SURVEY.md Appendix B (deterministic, no RNG)",
+            "config": {
+                "workload": f"{cfg.name}: {W}x{H}, {cfg.n_spheres} spheres + checkerboard, {cfg.n_lights} light(s), "
+                            f"{B} bounce(s), pitch 500/W; step = {frames} frame(s)",
+                "width": W, "height": H, "spheres": cfg.n_spheres, "lights": cfg.n_lights, "bounces": B,
+                "rays_per_frame": rays_frame, "frames_per_step": frames,
+                "parallelism": f"row-bands(h={args.band_height}) x {world} + RCCL gather" if world > 1 else "single GPU",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": "rt_render_kernel", "kernel_ms": round(avg_kern_ms, 5),
+                "algorithmic_bytes_per_launch": bytes_launch,
+            },
+            "roofline_fp64": {
+                "bound": "fp64-valu", "achieved": round(tflops, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(tflops / FP64_PEAK_TFLOPS, 4), "flops_per_launch": flops_launch,
+            },
+            "parity": parity,
+        }
+        if world == 1 and not args.no_cpu_baseline and not args.profile_kernel_only:
+            from oracle import pyoracle as po
+            nt = cpu_threads()
+            sa = scene.to_abi()
+            best = float("inf")
+            for _ in range(args.cpu_reps):
+                t = time.perf_counter()
+                po.render(sa, cam, W, H, B, nthreads=nt)
+                best = min(best, time.perf_counter() - t)
+            res["cpu_baseline"] = {
+                "value": round(rays_frame / best / 1e6, 3), "unit": "Mray/s", "cores": nt, "kind": "port",
+                "sample": f"full {cfg.name} frame ({W}x{H}, {rays_frame} rays) with oracle/rt_oracle.c "
+                          f"(bit-exact restatement, gcc -O2, OpenMP {nt} threads), best of {args.cpu_reps}; "
+                          f"{best * 1e3:.1f} ms/frame; host CPU: {cpu_model()}",
+            }
+        print(json.dumps(res), flush=True)
+    tr.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

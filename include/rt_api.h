@@ -1,0 +1,208 @@
+/*
+ * rt_api.h — C ABI of the MI355X-native per-pixel ray tracer.
+ *
+ * This is the drop-in boundary for the reference's frame hand-off:
+ *   draw()            Hw4/MySdlApplication.cpp:1541-1563  (builds lights + camera, calls L5)
+ *   rayTraceScreen()  Hw4/MySdlApplication.cpp:1251-1324  (camera basis, per-pixel rays, GL emit)
+ *   rayTraceRay()     Hw4/MySdlApplication.cpp:1184-1249  (closest hit, shadows, bounces)
+ *   Shape/Triangle/CheckerBoard::intersection  MySdlApplication.cpp:611-823, 1084-1113
+ * The reference has no plugin/FFI API: its seam is a C++ call made on the GL thread.
+ * This header replaces that call with plain C types: the scene is a flat descriptor built from the
+ * same inputs `loadScene` uses (MySdlApplication.cpp:1495-1539), pixels land in caller-owned buffers.
+ *
+ * Conventions
+ *  - All geometry is IEEE binary64, exactly as the reference's `Point` (MySdlApplication.cpp:136-212).
+ *  - Pixel (i, j) has j = 0 at the BOTTOM row (gluOrtho2D(0,W,0,H), MySdlApplication.cpp:1383) and is
+ *    stored at index j*W + i of a full image.  A row-banded call (rt_rows) stores its rows densely in
+ *    local order; rt_unshuffle_dev puts gathered bands back into image order.
+ *  - Every entry point returns RT_OK (0) or a negative RT_E* code; rt_last_error() gives the text for
+ *    the calling thread.  There is no silent fallback: without a HIP device every render call fails
+ *    with RT_EHIP.
+ *  - One rt_ctx per (thread, device).  A context owns the device copy of the scene; rt_render_dev is
+ *    asynchronous on the caller's stream and does not allocate, so it may be captured in a hipGraph.
+ */
+#ifndef RT_API_H
+#define RT_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+#define RT_OK            0
+#define RT_EINVAL       -1   /* bad argument (null pointer, size, unsupported material, ...) */
+#define RT_EHIP         -2   /* HIP runtime error or no device */
+#define RT_ENOMEM       -3   /* allocation failed */
+#define RT_EUNSUPPORTED -4   /* reference feature outside the GPU path (transparent materials, meshes) */
+
+#define RT_MAX_SPHERES 1024
+#define RT_MAX_LIGHTS  16
+#define RT_MAX_DEPTH   7     /* reference uses MAX_DEPTH = 5 (MySdlApplication.cpp:48) */
+
+/* Material — MySdlApplication.cpp:272-307 (ambient, diffuse, specular, transparency, refraction). */
+typedef struct rt_material {
+    double ambient[3];
+    double diffuse[3];
+    double specular[3];
+    double transparency[3];
+    double refraction;
+} rt_material;
+
+/* Sphere(p, r) — MySdlApplication.cpp:846-860.  `center` is scene-local, exactly the `p` handed to the
+ * reference constructor (e.g. convertStringCoordinate("d7")); the world centre is center + scene.position. */
+typedef struct rt_sphere {
+    double center[3];
+    double radius;
+} rt_sphere;
+
+/* Light(color, position) — MySdlApplication.cpp:214-232.  World coordinates. */
+typedef struct rt_light {
+    double color[3];
+    double position[3];
+} rt_light;
+
+/* The reference's g_scene (MySdlApplication.cpp:590) flattened: a bounding sphere at `position` of
+ * `radius`, then children in insertion order — the CheckerBoard first when present (initScene2 inserts
+ * it first, MySdlApplication.cpp:1442-1443), then the spheres in the order given. */
+typedef struct rt_scene {
+    double position[3];          /* g_scene position, BOARD_POSITION (MySdlApplication.cpp:42) */
+    double radius;               /* g_scene radius sqrt(3)*BOARD_HALF_SIZE; <= 0 disables the cull */
+    int32_t has_board;           /* CheckerBoard present */
+    int32_t n_spheres;           /* <= RT_MAX_SPHERES */
+    int32_t n_lights;            /* <= RT_MAX_LIGHTS */
+    int32_t reserved0;
+    double board_position[3];    /* CheckerBoard(p) argument (scene-local) */
+    double board_half_size;      /* BOARD_HALF_SIZE (MySdlApplication.cpp:44) */
+    double square_edge_size;     /* SQUARE_EDGE_SIZE (MySdlApplication.cpp:46) */
+    double small_number;         /* SMALL_NUMBER (MySdlApplication.cpp:50) */
+    double attenuation_factor;   /* ATTENUATION_FACTOR (MySdlApplication.cpp:35) */
+    rt_material white_square;    /* g_whiteSquare (MySdlApplication.cpp:583) */
+    rt_material black_square;    /* g_blackSquare (MySdlApplication.cpp:585) */
+    rt_material sphere_material; /* g_sphereMaterial (MySdlApplication.cpp:586) */
+    const rt_sphere* spheres;    /* host pointer, n_spheres entries */
+    const rt_light* lights;      /* host pointer, n_lights entries (the per-frame `lights` vector) */
+} rt_scene;
+
+/* Camera — rayTraceScreen's arguments (MySdlApplication.cpp:1251-1252, called at :1560).
+ * Primary ray of pixel (i, j): Line(eye, sp) with
+ *   sp = (look_at + (pitch*(double)(i + bottom_x))*right) + (pitch*(double)(j + bottom_y))*up'
+ * where right = normalize((look_at-eye) x up), up' = normalize(right x (look_at-eye))
+ * (MySdlApplication.cpp:1270-1279).  pitch = 1 is the reference's unit pixel step (:1315, :1321). */
+typedef struct rt_camera {
+    double eye[3];               /* CAMERA_POSITION (MySdlApplication.cpp:38) */
+    double look_at[3];           /* LOOK_AT_VECTOR (MySdlApplication.cpp:39) */
+    double up[3];                /* UP_VECTOR (MySdlApplication.cpp:40) */
+    double pitch;                /* world units between adjacent pixel centres */
+    int32_t bottom_x;            /* -W/2 (C integer division, MySdlApplication.cpp:1560) */
+    int32_t bottom_y;            /* -H/2 */
+} rt_camera;
+
+/* Row banding for multi-GPU sharding: the image's rows are cut into bands of `band_height` rows and
+ * band b goes to rank b % n_ranks.  A call renders only its rank's rows, densely, in increasing order.
+ * NULL rt_rows* (or n_ranks == 1) means the full image. */
+typedef struct rt_rows {
+    int32_t band_height;
+    int32_t n_ranks;
+    int32_t rank;
+    int32_t reserved0;
+} rt_rows;
+
+/* Ray counts actually traced (SURVEY.md §8d rule): primary segments, reflected segments (levels 1..B,
+ * only after a hit), shadow rays (one per light per hit). */
+typedef struct rt_stats {
+    uint64_t primary_rays;
+    uint64_t reflect_rays;
+    uint64_t shadow_rays;
+    double kernel_ms;
+} rt_stats;
+
+/* Per-ray hit record, the observable part of the reference's Intersection (MySdlApplication.cpp:309-359). */
+typedef struct rt_hit {
+    double point[3];
+    double normal[3];
+    double reflected_end[3];     /* reflectedRay().endPoint() = point + r */
+    int32_t hit;                 /* Intersection::intersects() */
+    int32_t material;            /* 0 white square, 1 black square, 2 sphere, -1 none */
+} rt_hit;
+
+typedef struct rt_ctx rt_ctx;
+
+/* ---- library / device ---------------------------------------------------------------------- */
+int rt_abi_version(void);
+const char* rt_last_error(void);
+int rt_device_count(int* count);
+int rt_ctx_create(int device, rt_ctx** out);
+int rt_ctx_destroy(rt_ctx* ctx);
+
+/* ---- scene (host side; no device needed) --------------------------------------------------- */
+/* Fill constants and materials with the reference's globals (MySdlApplication.cpp:31-52, 583-590):
+ * empty scene, board present at (0,0,0), no spheres, no lights. */
+int rt_scene_init_reference(rt_scene* scene);
+/* convertStringCoordinate (MySdlApplication.cpp:1326-1346): "b6" -> board-local point. */
+int rt_convert_string_coordinate(const char* square, double out[3]);
+/* Light placement used by loadScene (MySdlApplication.cpp:1511):
+ * BOARD_POSITION + (0, 3.5*SQUARE_EDGE_SIZE, 0) + convertStringCoordinate(square). */
+int rt_light_position_from_square(const char* square, double out[3]);
+/* loadScene (MySdlApplication.cpp:1495-1539) over boardMap entries (square -> type; types as the
+ * reference enum {LIGHT, TETRAHEDRON, CUBE, SPHERE, CYLINDER, CONE}, MySdlApplication.cpp:16).
+ * Duplicate squares keep the last type (boardMap[tmp] = type, :1467), entries are visited in
+ * std::map<string> order, the last light wins.  Spheres are written to sphere_buf (capacity
+ * sphere_cap); the light (white, g_lightColor) to *light.  Returns RT_EUNSUPPORTED if a mesh type
+ * (tetrahedron, cube, cylinder, cone) is present; spheres and light are still filled. */
+int rt_load_scene(const char* const* squares, const int32_t* types, int n, rt_scene* scene,
+                  rt_sphere* sphere_buf, int sphere_cap, rt_light* light);
+/* draw()'s camera (MySdlApplication.cpp:1556-1560) for a W x H window at the given pitch. */
+int rt_camera_init_reference(rt_camera* cam, int width, int height, double pitch);
+/* Number of image rows a rank renders under `rows` (NULL = all rows). */
+int rt_local_rows(int height, const rt_rows* rows, int* out);
+/* Global image row of local row `local_row` under `rows`. */
+int rt_global_row(int height, const rt_rows* rows, int local_row, int* out);
+
+/* ---- device path ---------------------------------------------------------------------------- */
+/* Validate and upload the scene (scene + spheres + lights are copied; caller keeps ownership). */
+int rt_set_scene(rt_ctx* ctx, const rt_scene* scene);
+
+/* Render this rank's rows of a width x height frame with `depth` bounces (rayTraceRay's `depth`).
+ * Device pointers, each nullable, each local_rows*width pixels:
+ *   rgba32f: float4 (r,g,b,1) unclamped, rgba8: clamp(c,0,1)*255 rounded (RGBA8 = floor(v*255+0.5)),
+ *   rgb64f: 3 doubles (the reference's double colour, for bit-exact parity),
+ *   raycount: per pixel packed (primary+reflect) | shadow << 16.
+ * `stream` is a hipStream_t (NULL = default stream).  Asynchronous; no allocation. */
+int rt_render_dev(rt_ctx* ctx, const rt_camera* cam, int width, int height, int depth,
+                  const rt_rows* rows, float* rgba32f, uint8_t* rgba8, double* rgb64f,
+                  uint32_t* raycount, void* stream);
+
+/* Synchronous host-buffer convenience: uploads `scene`, renders, copies back, fills *stats
+ * (ray counts + kernel time).  Any output pointer may be NULL. */
+int rt_render(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, int width, int height,
+              int depth, const rt_rows* rows, float* rgba32f, uint8_t* rgba8, double* rgb64f,
+              rt_stats* stats);
+
+/* Arbitrary rays (Line(start, end)) through the uploaded scene on the device:
+ * rt_intersect_dev = g_scene.intersection (MySdlApplication.cpp:724-823) -> rt_hit per ray;
+ * rt_trace_rays_dev = rayTraceRay(scene, lights, ray, color, depth) -> 3 doubles per ray. */
+int rt_intersect_dev(rt_ctx* ctx, const double* starts, const double* ends, int n, rt_hit* hits,
+                     void* stream);
+int rt_trace_rays_dev(rt_ctx* ctx, const double* starts, const double* ends, int n, int depth,
+                      double* rgb64f, uint32_t* raycount, void* stream);
+
+/* Put gathered bands back into image order: `gathered` holds n_ranks slabs, slab r = rank r's local
+ * rows (rt_local_rows rows each, slabs padded to `slab_rows` rows), `image` is height x width.
+ * elem_bytes in {1,2,4,8,16,24,32}: bytes per pixel. */
+int rt_unshuffle_dev(const void* gathered, void* image, int width, int height, int elem_bytes,
+                     int band_height, int n_ranks, int slab_rows, void* stream);
+
+/* ---- output (host) -------------------------------------------------------------------------- */
+/* writePpmScreenshot format (Hw4/ppm.cpp:15-25): "P6 W H 255\n" then RGB rows top-down, from an
+ * RGBA8 (or RGB8 when channels == 3) bottom-up image as glReadPixels returns it. */
+int rt_write_ppm(const char* path, const uint8_t* pixels, int width, int height, int channels);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_API_H */

@@ -1,0 +1,206 @@
+"""Python loader for the oracle libraries.  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module; the
+product package never does.
+
+* ``librt_oracle.so`` — the C restatement (oracle/rt_oracle.c), runs anywhere (also on the GPU box).
+* ``_ref/libref.so``  — the reference's own rayTraceRay compiled from /root/reference (oracle/Makefile
+  target ``ref``); exists only in the build container, never on the GPU box.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_uint32, c_uint64, c_void_p, c_size_t
+
+import numpy as np
+
+from ray_tracer_fragment_shader_amd import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "librt_oracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libref.so")
+REF_SRC = "/root/reference/Hw4/MySdlApplication.cpp"
+
+_oracle = None
+_ref = None
+
+
+def build(ref: bool = True) -> None:
+    """make the restatement (always) and the reference build (when /root/reference is present)."""
+    subprocess.run(["make", "-C", HERE, "all"], check=True, stdout=subprocess.DEVNULL)
+    if ref and os.path.exists(REF_SRC):
+        subprocess.run(["make", "-C", HERE, "ref"], check=True, stdout=subprocess.DEVNULL)
+
+
+def oracle() -> ctypes.CDLL:
+    global _oracle
+    if _oracle is None:
+        if not os.path.exists(ORACLE_SO):
+            build(ref=False)
+        L = ctypes.CDLL(ORACLE_SO)
+        L.oracle_render.restype = c_int
+        L.oracle_render.argtypes = [POINTER(abi.rt_scene), POINTER(abi.rt_camera), c_int, c_int, c_int,
+                                    POINTER(abi.rt_rows), c_void_p, c_void_p, c_int]
+        L.oracle_trace_rays.restype = c_int
+        L.oracle_trace_rays.argtypes = [POINTER(abi.rt_scene), c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                        c_void_p, c_int]
+        L.oracle_intersect.restype = c_int
+        L.oracle_intersect.argtypes = [POINTER(abi.rt_scene), c_void_p, c_void_p, c_int, POINTER(abi.rt_hit)]
+        L.oracle_camera_basis.restype = None
+        L.oracle_camera_basis.argtypes = [POINTER(abi.rt_camera), c_void_p, c_void_p]
+        L.oracle_local_rows.restype = c_int
+        L.oracle_local_rows.argtypes = [c_int, POINTER(abi.rt_rows)]
+        L.oracle_convert_string_coordinate.restype = None
+        L.oracle_convert_string_coordinate.argtypes = [c_char_p, c_void_p]
+        L.oracle_fnv1a64.restype = c_uint64
+        L.oracle_fnv1a64.argtypes = [c_void_p, c_size_t]
+        _oracle = L
+    return _oracle
+
+
+def ref_available() -> bool:
+    return os.path.exists(REF_SO) or os.path.exists(REF_SRC)
+
+
+def ref() -> ctypes.CDLL:
+    global _ref
+    if _ref is None:
+        if not os.path.exists(REF_SO):
+            if not os.path.exists(REF_SRC):
+                raise RuntimeError("reference build unavailable (no /root/reference here)")
+            build(ref=True)
+        L = ctypes.CDLL(REF_SO)
+        scene_args = [c_char_p, c_void_p, c_void_p, c_int, c_char_p, c_void_p, c_int]
+        L.ref_render.restype = c_int
+        L.ref_render.argtypes = scene_args + [c_int, c_int, c_int, c_double, c_int, c_int, c_void_p, c_int]
+        L.ref_render_pixels.restype = c_int
+        L.ref_render_pixels.argtypes = scene_args + [c_int, c_int, c_int, c_double, c_void_p, c_void_p, c_int,
+                                                     c_void_p, c_int]
+        L.ref_trace_rays.restype = c_int
+        L.ref_trace_rays.argtypes = scene_args + [c_void_p, c_void_p, c_int, c_int, c_void_p]
+        L.ref_intersect.restype = c_int
+        L.ref_intersect.argtypes = [c_char_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                    c_void_p, c_void_p]
+        L.ref_convert_string_coordinate.restype = None
+        L.ref_convert_string_coordinate.argtypes = [c_char_p, c_void_p]
+        _ref = L
+    return _ref
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def fnv1a64(a: np.ndarray) -> int:
+    a = np.ascontiguousarray(a)
+    return int(oracle().oracle_fnv1a64(_ptr(a), a.nbytes))
+
+
+# ---------------------------------------------------------------------------------------- restatement
+def render(scene_abi, cam, width, height, depth, rows=None, nthreads=0):
+    """-> (rgb float64 [local_rows, W, 3], raycount uint32 [local_rows, W])"""
+    L = oracle()
+    nl = L.oracle_local_rows(height, ctypes.byref(rows) if rows is not None else None)
+    rgb = np.zeros((nl, width, 3), np.float64)
+    rc = np.zeros((nl, width), np.uint32)
+    code = L.oracle_render(ctypes.byref(scene_abi), ctypes.byref(cam), width, height, depth,
+                           ctypes.byref(rows) if rows is not None else None, _ptr(rgb), _ptr(rc), nthreads)
+    if code:
+        raise RuntimeError(f"oracle_render failed: {code}")
+    return rgb, rc
+
+
+def trace_rays(scene_abi, starts, ends, depth, nthreads=0):
+    starts = np.ascontiguousarray(starts, np.float64)
+    ends = np.ascontiguousarray(ends, np.float64)
+    n = starts.shape[0]
+    rgb = np.zeros((n, 3), np.float64)
+    rc = np.zeros(n, np.uint32)
+    code = oracle().oracle_trace_rays(ctypes.byref(scene_abi), _ptr(starts), _ptr(ends), n, depth, _ptr(rgb),
+                                      _ptr(rc), nthreads)
+    if code:
+        raise RuntimeError(f"oracle_trace_rays failed: {code}")
+    return rgb, rc
+
+
+def intersect(scene_abi, starts, ends):
+    """-> dict of arrays: hit, material, point, normal, reflected_end"""
+    starts = np.ascontiguousarray(starts, np.float64)
+    ends = np.ascontiguousarray(ends, np.float64)
+    n = starts.shape[0]
+    hits = (abi.rt_hit * max(n, 1))()
+    code = oracle().oracle_intersect(ctypes.byref(scene_abi), _ptr(starts), _ptr(ends), n, hits)
+    if code:
+        raise RuntimeError(f"oracle_intersect failed: {code}")
+    return hits_to_dict(hits, n)
+
+
+def hits_to_dict(hits, n):
+    raw = np.frombuffer(hits, dtype=np.uint8, count=n * ctypes.sizeof(abi.rt_hit)).reshape(n, -1)
+    d = raw[:, :72].copy().view(np.float64).reshape(n, 9)
+    i = raw[:, 72:80].copy().view(np.int32).reshape(n, 2)
+    return {"point": d[:, 0:3], "normal": d[:, 3:6], "reflected_end": d[:, 6:9], "hit": i[:, 0],
+            "material": i[:, 1]}
+
+
+def camera_basis(cam):
+    r = np.zeros(3)
+    u = np.zeros(3)
+    oracle().oracle_camera_basis(ctypes.byref(cam), _ptr(r), _ptr(u))
+    return r, u
+
+
+def screen_points(cam, width, height, rows=None):
+    """Primary-ray end points sp(i, j) of SURVEY.md Appendix B, computed with numpy in the same operation
+    order (IEEE float64, elementwise: bit-identical to the C code)."""
+    right, upp = camera_basis(cam)
+    look = np.array(cam.look_at[:])
+    js = np.arange(height)
+    if rows is not None and rows.n_ranks > 1:
+        js = js[(js // rows.band_height) % rows.n_ranks == rows.rank]
+    ii = np.arange(width)
+    a = cam.pitch * (ii + cam.bottom_x).astype(np.float64)
+    b = cam.pitch * (js + cam.bottom_y).astype(np.float64)
+    sp = (look[None, None, :] + a[None, :, None] * right[None, None, :]) + b[:, None, None] * upp[None, None, :]
+    return sp
+
+
+# ------------------------------------------------------------------------------------- reference build
+def ref_render(scene, width, height, depth, pitch, row_begin=0, row_end=None, nthreads=0):
+    row_end = height if row_end is None else row_end
+    rgb = np.zeros((row_end - row_begin, width, 3), np.float64)
+    ref().ref_render(*scene.ref_args(), width, height, depth, float(pitch), row_begin, row_end, _ptr(rgb),
+                     nthreads)
+    return rgb
+
+
+def ref_render_pixels(scene, width, height, depth, pitch, pi, pj, nthreads=0):
+    pi = np.ascontiguousarray(pi, np.int32)
+    pj = np.ascontiguousarray(pj, np.int32)
+    rgb = np.zeros((pi.shape[0], 3), np.float64)
+    ref().ref_render_pixels(*scene.ref_args(), width, height, depth, float(pitch), _ptr(pi), _ptr(pj),
+                            pi.shape[0], _ptr(rgb), nthreads)
+    return rgb
+
+
+def ref_trace_rays(scene, starts, ends, depth):
+    starts = np.ascontiguousarray(starts, np.float64)
+    ends = np.ascontiguousarray(ends, np.float64)
+    rgb = np.zeros((starts.shape[0], 3), np.float64)
+    ref().ref_trace_rays(*scene.ref_args(), _ptr(starts), _ptr(ends), starts.shape[0], depth, _ptr(rgb))
+    return rgb
+
+
+def ref_intersect(scene, starts, ends):
+    starts = np.ascontiguousarray(starts, np.float64)
+    ends = np.ascontiguousarray(ends, np.float64)
+    n = starts.shape[0]
+    out9 = np.zeros((n, 9), np.float64)
+    hit = np.zeros(n, np.int32)
+    mat = np.zeros(n, np.int32)
+    a = scene.ref_args()
+    ref().ref_intersect(a[0], a[1], a[2], a[3], _ptr(starts), _ptr(ends), n, _ptr(out9), _ptr(hit), _ptr(mat))
+    return {"point": out9[:, 0:3], "normal": out9[:, 3:6], "reflected_end": out9[:, 6:9], "hit": hit,
+            "material": mat}

@@ -1,0 +1,150 @@
+// ref_harness.cpp — TEST INFRASTRUCTURE (oracle/_ref build only; appended after the reference's own
+// hot-path source ranges by oracle/Makefile, so every class and function used below is the reference's).
+//
+// Scenes are built exactly the way the reference app builds them (loadScene, MySdlApplication.cpp:
+// 1495-1539): a g_scene-like Shape (:590), CheckerBoard(Point(0,0,0)) first (:1442-1443), then
+// Sphere(convertStringCoordinate(sq) [+ (0,yoff,0)], r) in order, Light(color, BOARD_POSITION +
+// (0,3.5*SQUARE_EDGE_SIZE,0) + convertStringCoordinate(sq)) (:1511).  Pixels use the deterministic
+// primary ray of SURVEY.md Appendix B with the rayTraceScreen basis (:1270-1279) and are shaded by the
+// reference rayTraceRay (:1184-1249).
+#include <omp.h>
+#include <cstdint>
+
+namespace {
+
+struct RefScene {
+    Shape* scene;
+    vector<Light> lights;
+};
+
+RefScene build(const char* sph_sq, const double* sph_yoff, const double* sph_r, int n_sph,
+               const char* light_sq, const double* light_col, int n_lights) {
+    RefScene r;
+    r.scene = new Shape(Point(BOARD_POSITION), Material(), sqrt((double)3) * BOARD_HALF_SIZE, false);
+    r.scene->addRayObject(new CheckerBoard(Point(0.0, 0.0, 0.0)));
+    for (int k = 0; k < n_sph; ++k) {
+        string sq(sph_sq + 2 * k, 2);
+        Point c = convertStringCoordinate(sq);
+        if (sph_yoff) c = c + Point(0.0, sph_yoff[k], 0.0);
+        r.scene->addRayObject(new Sphere(c, sph_r[k]));
+    }
+    for (int k = 0; k < n_lights; ++k) {
+        string sq(light_sq + 2 * k, 2);
+        Point pos = Point(BOARD_POSITION) + Point(0.0, 3.5 * SQUARE_EDGE_SIZE, 0.0) + convertStringCoordinate(sq);
+        r.lights.push_back(Light(Point(light_col + 3 * k), pos));
+    }
+    return r;
+}
+
+int material_id(Material m) {
+    if (m.specular().x() == 0) return 1;          // g_blackSquare
+    if (m.ambient().x() != 0) return 0;           // g_whiteSquare
+    return 2;                                     // g_sphereMaterial
+}
+
+}  // namespace
+
+extern "C" {
+
+// Render rows [row_begin, row_end) of a W x H frame; rgb has (row_end-row_begin)*W*3 doubles.
+int ref_render(const char* sph_sq, const double* sph_yoff, const double* sph_r, int n_sph,
+               const char* light_sq, const double* light_col, int n_lights, int W, int H, int depth,
+               double pitch, int row_begin, int row_end, double* rgb, int nthreads) {
+    RefScene rs = build(sph_sq, sph_yoff, sph_r, n_sph, light_sq, light_col, n_lights);
+    Point camera(CAMERA_POSITION);
+    Point lookAt(LOOK_AT_VECTOR);
+    Point up(UP_VECTOR);
+    Point lookDirection = lookAt - camera;          // rayTraceScreen basis, :1270-1277
+    Point right = lookDirection * up;
+    right.normalize();
+    up = right * lookDirection;
+    up.normalize();
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int j = row_begin; j < row_end; ++j) {
+        for (int i = 0; i < W; ++i) {
+            Point sp = (lookAt + (pitch * (double)(i - W / 2)) * right) + (pitch * (double)(j - H / 2)) * up;
+            Point color(0.0, 0.0, 0.0);
+            rayTraceRay(*rs.scene, rs.lights, Line(camera, sp), color, (unsigned)depth);
+            size_t k = ((size_t)(j - row_begin) * W + i) * 3;
+            rgb[k] = color.x(); rgb[k + 1] = color.y(); rgb[k + 2] = color.z();
+        }
+    }
+    delete rs.scene;
+    return 0;
+}
+
+// Sampled pixels (i[k], j[k]) of a W x H frame.
+int ref_render_pixels(const char* sph_sq, const double* sph_yoff, const double* sph_r, int n_sph,
+                      const char* light_sq, const double* light_col, int n_lights, int W, int H,
+                      int depth, double pitch, const int32_t* pi, const int32_t* pj, int n,
+                      double* rgb, int nthreads) {
+    RefScene rs = build(sph_sq, sph_yoff, sph_r, n_sph, light_sq, light_col, n_lights);
+    Point camera(CAMERA_POSITION);
+    Point lookAt(LOOK_AT_VECTOR);
+    Point up(UP_VECTOR);
+    Point lookDirection = lookAt - camera;
+    Point right = lookDirection * up;
+    right.normalize();
+    up = right * lookDirection;
+    up.normalize();
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int k = 0; k < n; ++k) {
+        int i = pi[k], j = pj[k];
+        Point sp = (lookAt + (pitch * (double)(i - W / 2)) * right) + (pitch * (double)(j - H / 2)) * up;
+        Point color(0.0, 0.0, 0.0);
+        rayTraceRay(*rs.scene, rs.lights, Line(camera, sp), color, (unsigned)depth);
+        rgb[3 * k] = color.x(); rgb[3 * k + 1] = color.y(); rgb[3 * k + 2] = color.z();
+    }
+    delete rs.scene;
+    return 0;
+}
+
+// rayTraceRay on arbitrary rays Line(starts[k], ends[k]).
+int ref_trace_rays(const char* sph_sq, const double* sph_yoff, const double* sph_r, int n_sph,
+                   const char* light_sq, const double* light_col, int n_lights, const double* starts,
+                   const double* ends, int n, int depth, double* rgb) {
+    RefScene rs = build(sph_sq, sph_yoff, sph_r, n_sph, light_sq, light_col, n_lights);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int k = 0; k < n; ++k) {
+        Point color(0.0, 0.0, 0.0);
+        rayTraceRay(*rs.scene, rs.lights, Line(Point(starts + 3 * k), Point(ends + 3 * k)), color,
+                    (unsigned)depth);
+        rgb[3 * k] = color.x(); rgb[3 * k + 1] = color.y(); rgb[3 * k + 2] = color.z();
+    }
+    delete rs.scene;
+    return 0;
+}
+
+// g_scene.intersection(ray, Point(0,0,0), inter) on arbitrary rays: per ray 9 doubles
+// (point, normal, reflectedRay end) + hit flag + material id.
+int ref_intersect(const char* sph_sq, const double* sph_yoff, const double* sph_r, int n_sph,
+                  const double* starts, const double* ends, int n, double* out9, int32_t* hit,
+                  int32_t* mat) {
+    RefScene rs = build(sph_sq, sph_yoff, sph_r, n_sph, "", nullptr, 0);
+    for (int k = 0; k < n; ++k) {
+        Intersection in;
+        rs.scene->intersection(Line(Point(starts + 3 * k), Point(ends + 3 * k)), Point(0.0, 0.0, 0.0), in);
+        hit[k] = in.intersects() ? 1 : 0;
+        mat[k] = -1;
+        for (int q = 0; q < 9; ++q) out9[9 * k + q] = 0.0;
+        if (hit[k]) {
+            Point p = in.point(), nn = in.normal(), e = in.reflectedRay().endPoint();
+            out9[9 * k + 0] = p.x(); out9[9 * k + 1] = p.y(); out9[9 * k + 2] = p.z();
+            out9[9 * k + 3] = nn.x(); out9[9 * k + 4] = nn.y(); out9[9 * k + 5] = nn.z();
+            out9[9 * k + 6] = e.x(); out9[9 * k + 7] = e.y(); out9[9 * k + 8] = e.z();
+            mat[k] = material_id(in.material());
+        }
+    }
+    delete rs.scene;
+    return 0;
+}
+
+// convertStringCoordinate (:1326-1346).
+void ref_convert_string_coordinate(const char* sq, double out[3]) {
+    Point p = convertStringCoordinate(string(sq, 2));
+    out[0] = p.x(); out[1] = p.y(); out[2] = p.z();
+}
+
+}  // extern "C"

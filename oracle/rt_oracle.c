@@ -1,0 +1,455 @@
+/*
+ * rt_oracle.c — CPU restatement of the reference ray tracer.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and
+ * only as the checker / the timed CPU baseline.  The product path (ray_tracer_fragment_shader_amd)
+ * never links or calls it.
+ *
+ * What it restates (all citations into /root/reference/Hw4/MySdlApplication.cpp):
+ *   Point ops                  :136-212, operator*(scalar,Point) :1118-1146
+ *   Line::direction/length     :258-269
+ *   Triangle ctor              :406-433      Triangle::intersection  :611-707
+ *   Shape::intersection        :724-823      (bounding sphere, sphere, composite closest hit)
+ *   Quad                       :826-843      (2 triangles, first hit wins)
+ *   CheckerBoard::intersection :1084-1113
+ *   attenuation                :1171-1182    rayTraceRay :1184-1249 (recursive, as the reference)
+ *   rayTraceScreen basis       :1270-1279    convertStringCoordinate :1326-1346
+ * The structure deliberately follows the reference (recursion, composite walk, closest hit for shadow
+ * rays) rather than the GPU kernel's iterative / any-hit form, so the two are independent.
+ *
+ * Parity pinning: this restatement is checked bit-for-bit against the reference's own rayTraceRay
+ * compiled from /root/reference (oracle/Makefile target `ref`, outputs in oracle/_ref/) and against the
+ * committed fixtures in tests/golden/ generated from it (tests/golden/make_golden.py).
+ *
+ * Build: gcc -O2 -ffp-contract=off -fopenmp (see oracle/Makefile).  No FMA contraction, IEEE sqrt/div.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/rt_api.h"
+
+/* ---------------------------------------------------------------- Point (MySdlApplication.cpp:136-212) */
+typedef struct { double x, y, z; } P;
+
+static inline P pt(double x, double y, double z) { P p = {x, y, z}; return p; }
+static inline P add(P a, P b) { return pt(a.x + b.x, a.y + b.y, a.z + b.z); }          /* :196-197 */
+static inline P sub(P a, P b) { return pt(a.x - b.x, a.y - b.y, a.z - b.z); }          /* :199-200 */
+static inline P scl(double s, P a) { return pt(s * a.x, s * a.y, s * a.z); }           /* :1118-1131 */
+static inline P had(P a, P b) { return pt(a.x * b.x, a.y * b.y, a.z * b.z); }          /* :192-193 */
+static inline double dot(P a, P b) { return a.x * b.x + a.y * b.y + a.z * b.z; }       /* :189-190 */
+static inline P cross(P a, P b) {                                                     /* :186-187 */
+    return pt(a.y * b.z - b.y * a.z, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static inline double len(P a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }     /* :174 */
+static inline P nrm(P a) { double l = len(a); return pt(a.x / l, a.y / l, a.z / l); }  /* :175 */
+static inline int is_zero(P a) { return a.x == 0 && a.y == 0 && a.z == 0; }           /* :173 */
+static inline P from3(const double* v) { return pt(v[0], v[1], v[2]); }
+
+/* Line (:234-270): direction = normalize(end - start), length = |end - start|. */
+typedef struct { P s, e; } Line;
+static inline P line_dir(Line l) { return nrm(sub(l.e, l.s)); }
+static inline double line_len(Line l) { return len(sub(l.e, l.s)); }
+
+typedef struct { P amb, diff, spec, transp; double refr; } Mat;
+
+static Mat mat_from(const rt_material* m) {
+    Mat r;
+    r.amb = from3(m->ambient); r.diff = from3(m->diffuse); r.spec = from3(m->specular);
+    r.transp = from3(m->transparency); r.refr = m->refraction;
+    return r;
+}
+
+/* Intersection (:309-359) — the fields rayTraceRay reads. */
+typedef struct {
+    int hit;
+    P point, normal;
+    Mat mat;
+    int mat_id;
+    Line refl, trans;
+} Inter;
+
+/* ---------------------------------------------------------------- Triangle (:380-437, :611-707) */
+typedef struct {
+    P pos;                    /* RayObject::_position (zero for the board's triangles, :838-841) */
+    P v0, v1, v2, u, v, n;
+    double uv, uu, vv, den;
+    int degenerate;
+    Mat mat;
+} Tri;
+
+static void tri_init(Tri* t, P pos, Mat m, P p1, P p2, P p3, double eps) {  /* ctor :406-433 */
+    t->pos = pos; t->mat = m;
+    t->v0 = p1; t->v1 = p2; t->v2 = p3;
+    t->u = sub(t->v1, t->v0);
+    t->v = sub(t->v2, t->v0);
+    t->n = cross(t->u, t->v);
+    t->degenerate = len(t->n) < eps;
+    t->n = nrm(t->n);
+    t->uv = dot(t->u, t->v);
+    t->uu = dot(t->u, t->u);
+    t->vv = dot(t->v, t->v);
+    t->den = t->uv * t->uv - t->uu * t->vv;
+    if (fabs(t->den) < eps) t->degenerate = 1;
+}
+
+static void tri_intersect(const Tri* t, Line ray, P off, double eps, Inter* in) {  /* :611-707 */
+    if (t->degenerate) { in->hit = 0; return; }
+    P position = add(t->pos, off);
+    P v0 = add(position, t->v0);
+    P p0 = ray.s, p1 = ray.e;
+    P diffP = sub(p1, p0);
+    double ndiffP = dot(t->n, diffP);
+    if (fabs(ndiffP) < eps) { in->hit = 0; return; }
+    double m = dot(t->n, sub(v0, p0)) / dot(t->n, diffP);
+    if (m < eps) { in->hit = 0; return; }
+    P p = add(p0, scl(m, diffP));
+    P w = sub(p, v0);
+    double wu = dot(w, t->u), wv = dot(w, t->v);
+    double s = (t->uv * wv - t->vv * wu) / t->den;
+    double tt = (t->uv * wu - t->uu * wv) / t->den;
+    if (s >= 0 && tt >= 0 && s + tt <= 1) {
+        P u = nrm(diffP);
+        P r = sub(u, scl(2 * dot(u, t->n), t->n));
+        double rr = t->mat.refr;
+        P tv = pt(0.0, 0.0, 0.0);
+        double cti = dot(u, t->n);
+        double modulus = 1 - rr * rr * (1 - cti * cti);
+        if (modulus > 0) {
+            double ctr = sqrt(modulus);
+            tv = sub(scl(rr, u), scl(ctr + rr * cti, t->n));
+        }
+        in->hit = 1; in->point = p; in->normal = t->n; in->mat = t->mat; in->mat_id = -1;
+        in->refl.s = p; in->refl.e = add(p, r);
+        in->trans.s = p; in->trans.e = add(p, tv);
+    } else {
+        in->hit = 0;
+    }
+}
+
+/* ---------------------------------------------------------------- scene = g_scene (:590) */
+typedef struct {
+    P pos;            /* Sphere's _position (scene-local) */
+    double radius;
+    Mat mat;
+} Sph;
+
+typedef struct {
+    P position;       /* g_scene _position */
+    double radius;    /* g_scene _radius (bounding sphere) */
+    double eps, att;
+    int has_board;
+    P board_p;        /* CheckerBoard(p): the Quad's _position (:1066) */
+    Tri board_tri[2]; /* Quad(p, Material(), ...) sub-triangles (:826-843, :1066-1069) */
+    double half, square;
+    Mat white, black;
+    int n_sph;
+    Sph* sph;
+    int n_lights;
+    P lcol[RT_MAX_LIGHTS], lpos[RT_MAX_LIGHTS];
+} Scene;
+
+static int scene_build(const rt_scene* d, Scene* s) {
+    memset(s, 0, sizeof(*s));
+    if (d->n_spheres < 0 || d->n_lights < 0 || d->n_lights > RT_MAX_LIGHTS) return RT_EINVAL;
+    s->position = from3(d->position);
+    s->radius = d->radius;
+    s->eps = d->small_number;
+    s->att = d->attenuation_factor;
+    s->has_board = d->has_board;
+    s->board_p = from3(d->board_position);
+    s->half = d->board_half_size;
+    s->square = d->square_edge_size;
+    s->white = mat_from(&d->white_square);
+    s->black = mat_from(&d->black_square);
+    {
+        double h = s->half;
+        Mat def; /* Material() (:291-293) */
+        def.amb = pt(0.0, 0.0, 0.0); def.diff = def.amb; def.spec = def.amb; def.transp = def.amb;
+        def.refr = 1;
+        P p1 = pt(-h, 0, -h), p2 = pt(h, 0, -h), p3 = pt(h, 0, h), p4 = pt(-h, 0, h);
+        P zero = pt(0.0, 0.0, 0.0);
+        tri_init(&s->board_tri[0], zero, def, p1, p2, p3, s->eps);
+        tri_init(&s->board_tri[1], zero, def, p1, p3, p4, s->eps);
+    }
+    s->n_sph = d->n_spheres;
+    s->sph = (Sph*)calloc((size_t)(d->n_spheres > 0 ? d->n_spheres : 1), sizeof(Sph));
+    if (!s->sph) return RT_ENOMEM;
+    Mat sm = mat_from(&d->sphere_material);
+    for (int k = 0; k < d->n_spheres; ++k) {
+        s->sph[k].pos = from3(d->spheres[k].center);
+        s->sph[k].radius = d->spheres[k].radius;
+        s->sph[k].mat = sm;
+    }
+    s->n_lights = d->n_lights;
+    for (int k = 0; k < d->n_lights; ++k) {
+        s->lcol[k] = from3(d->lights[k].color);
+        s->lpos[k] = from3(d->lights[k].position);
+    }
+    return RT_OK;
+}
+
+static void scene_free(Scene* s) { free(s->sph); s->sph = NULL; }
+
+/* Quad = Shape(p, m, 0, false, true): no bound test (radius 0), first hit returns (:817). */
+static void quad_intersect(const Scene* s, Line ray, P off, Inter* in) {
+    P position = add(s->board_p, off);          /* Shape::intersection :739 */
+    in->hit = 0;
+    double minDistance = -1.0;
+    for (int i = 0; i < 2; ++i) {
+        Inter tmp;
+        tri_intersect(&s->board_tri[i], ray, position, s->eps, &tmp);
+        if (tmp.hit) {
+            double d = len(sub(tmp.point, ray.s));
+            if (d < minDistance || minDistance < 0.0) {
+                minDistance = d;
+                *in = tmp;
+                return;                          /* _canIntersectOnlyOneSubObject */
+            }
+        }
+    }
+}
+
+static void board_intersect(const Scene* s, Line ray, P off, Inter* in) {  /* :1084-1113 */
+    quad_intersect(s, ray, off, in);
+    if (in->hit) {
+        P p = add(sub(in->point, off), pt(s->half, 0, s->half));
+        int squareSum = (int)(p.x / s->square) + (int)(p.z / s->square);
+        if ((squareSum & 1) == 0) { in->mat = s->white; in->mat_id = 0; }
+        else { in->mat = s->black; in->mat_id = 1; }
+    }
+}
+
+static void sphere_intersect(const Sph* sp, Line ray, P off, double eps, Inter* in) {  /* :737-793 */
+    P u = line_dir(ray);
+    P p0 = ray.s;
+    P position = add(sp->pos, off);
+    P deltaP = sub(position, p0);
+    double uDeltaP = dot(u, deltaP);
+    double disc = uDeltaP * uDeltaP - dot(deltaP, deltaP) + sp->radius * sp->radius;
+    double s = uDeltaP - sqrt(disc);
+    if (disc < 0 || fabs(s) < eps) { in->hit = 0; return; }
+    P p = add(p0, scl(s, u));
+    P dirP0 = sub(p, position);
+    if (s < eps) { in->hit = 0; return; }
+    P n = nrm(dirP0);
+    P r = sub(u, scl(2 * dot(u, n), n));
+    double rr = sp->mat.refr;
+    P tv = pt(0.0, 0.0, 0.0);
+    double cti = dot(u, n);
+    double modulus = 1 - rr * rr * (1 - cti * cti);
+    if (modulus > 0) {
+        double ctr = sqrt(modulus);
+        tv = sub(scl(rr, u), scl(ctr + rr * cti, n));
+    }
+    in->hit = 1; in->point = p; in->normal = n; in->mat = sp->mat; in->mat_id = 2;
+    in->refl.s = p; in->refl.e = add(p, r);
+    in->trans.s = p; in->trans.e = add(p, tv);
+}
+
+/* g_scene.intersection(ray, Point(0,0,0), inter): bounding sphere then closest child (:724-823). */
+static void scene_intersect(const Scene* s, Line ray, Inter* in) {
+    P off = pt(0.0, 0.0, 0.0);
+    P u = line_dir(ray);
+    P p0 = ray.s;
+    P position = add(s->position, off);
+    P deltaP = sub(position, p0);
+    if (s->radius > 0) {
+        double uDeltaP = dot(u, deltaP);
+        double disc = uDeltaP * uDeltaP - dot(deltaP, deltaP) + s->radius * s->radius;
+        double sv = uDeltaP - sqrt(disc);
+        if (disc < 0 || fabs(sv) < s->eps) { in->hit = 0; return; }
+    }
+    in->hit = 0;
+    double minDistance = -1.0;
+    int nchild = s->has_board + s->n_sph;
+    for (int c = 0; c < nchild; ++c) {
+        Inter tmp;
+        if (s->has_board && c == 0) board_intersect(s, ray, position, &tmp);
+        else sphere_intersect(&s->sph[c - s->has_board], ray, position, s->eps, &tmp);
+        if (tmp.hit) {
+            double d = len(sub(tmp.point, p0));
+            if (d < minDistance || minDistance < 0.0) {
+                minDistance = d;
+                *in = tmp;
+            }
+        }
+    }
+}
+
+static inline double attenuation(double att, double d) { return att / (att + d * d); }  /* :1171-1182 */
+
+typedef struct { uint32_t seg, shadow; } Count;
+
+/* rayTraceRay (:1184-1249), recursive exactly as the reference. */
+static void ray_trace_ray(const Scene* s, Line ray, P* color, unsigned depth, Count* cnt) {
+    Inter in;
+    cnt->seg++;
+    scene_intersect(s, ray, &in);
+    if (!in.hit) return;
+    P ptv = in.point;
+    Mat m = in.mat;
+    for (int i = 0; i < s->n_lights; ++i) {
+        Line sh; sh.s = ptv; sh.e = s->lpos[i];
+        Inter si;
+        cnt->shadow++;
+        scene_intersect(s, sh, &si);
+        if (!si.hit || !is_zero(si.mat.transp)) {
+            P lC = scl(attenuation(s->att, line_len(sh)), s->lcol[i]);
+            P term = add(add(had(m.amb, lC), scl(fabs(dot(in.normal, line_dir(sh))), had(m.diff, lC))),
+                         scl(fabs(dot(line_dir(ray), line_dir(in.refl))), had(m.spec, lC)));
+            *color = add(*color, term);
+        }
+    }
+    if (depth > 0) {
+        P tc = pt(0.0, 0.0, 0.0), rc = pt(0.0, 0.0, 0.0);
+        P transparency = m.transp;
+        P opacity = sub(pt(1.0, 1.0, 1.0), transparency);
+        if (!is_zero(transparency) && len(transparency) > s->eps) {
+            ray_trace_ray(s, in.trans, &tc, depth - 1, cnt);
+            *color = add(*color, had(transparency, tc));
+        }
+        if (!is_zero(opacity)) {
+            ray_trace_ray(s, in.refl, &rc, depth - 1, cnt);
+            *color = add(*color, had(opacity, rc));
+        }
+    }
+}
+
+/* ---------------------------------------------------------------- exported oracle entry points */
+
+/* rayTraceScreen basis (:1270-1279): right = normalize(LD x up); up' = normalize(right x LD). */
+void oracle_camera_basis(const rt_camera* c, double right[3], double upp[3]) {
+    P cam = from3(c->eye), look = from3(c->look_at), up = from3(c->up);
+    P ld = sub(look, cam);
+    P r = nrm(cross(ld, up));
+    P u = nrm(cross(r, ld));
+    right[0] = r.x; right[1] = r.y; right[2] = r.z;
+    upp[0] = u.x; upp[1] = u.y; upp[2] = u.z;
+}
+
+/* Screen point of pixel (i, j) — SURVEY.md Appendix B, the parity contract's primary ray. */
+static P screen_point(const rt_camera* c, P right, P upp, int i, int j) {
+    P look = from3(c->look_at);
+    return add(add(look, scl(c->pitch * (double)(i + c->bottom_x), right)),
+               scl(c->pitch * (double)(j + c->bottom_y), upp));
+}
+
+static int local_rows(int H, const rt_rows* r) {
+    if (!r || r->n_ranks <= 1) return H;
+    int hb = r->band_height, G = r->n_ranks, n = 0;
+    for (int j = 0; j < H; ++j) if ((j / hb) % G == r->rank) ++n;
+    return n;
+}
+
+static int global_row(const rt_rows* r, int lr) {
+    if (!r || r->n_ranks <= 1) return lr;
+    int hb = r->band_height, G = r->n_ranks;
+    int band = lr / hb, within = lr % hb;
+    return (band * G + r->rank) * hb + within;
+}
+
+int oracle_local_rows(int H, const rt_rows* r) { return local_rows(H, r); }
+
+/* Render rows of a W x H frame: rgb (3 doubles / pixel, local row order), raycount packed as in
+ * rt_render_dev.  nthreads <= 0 uses the OpenMP default. */
+int oracle_render(const rt_scene* d, const rt_camera* c, int W, int H, int depth, const rt_rows* rows,
+                  double* rgb, uint32_t* raycount, int nthreads) {
+    if (!d || !c || W <= 0 || H <= 0 || depth < 0) return RT_EINVAL;
+    Scene s;
+    int rc = scene_build(d, &s);
+    if (rc) { scene_free(&s); return rc; }
+    double rv[3], uv[3];
+    oracle_camera_basis(c, rv, uv);
+    P right = from3(rv), upp = from3(uv), cam = from3(c->eye);
+    int nl = local_rows(H, rows);
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int lr = 0; lr < nl; ++lr) {
+        int j = global_row(rows, lr);
+        for (int i = 0; i < W; ++i) {
+            Line ray; ray.s = cam; ray.e = screen_point(c, right, upp, i, j);
+            P col = pt(0.0, 0.0, 0.0);
+            Count cnt = {0, 0};
+            ray_trace_ray(&s, ray, &col, (unsigned)depth, &cnt);
+            size_t k = (size_t)lr * W + i;
+            if (rgb) { rgb[3 * k] = col.x; rgb[3 * k + 1] = col.y; rgb[3 * k + 2] = col.z; }
+            if (raycount) raycount[k] = cnt.seg | (cnt.shadow << 16);
+        }
+    }
+    scene_free(&s);
+    return RT_OK;
+}
+
+/* rayTraceRay on arbitrary rays. */
+int oracle_trace_rays(const rt_scene* d, const double* starts, const double* ends, int n, int depth,
+                      double* rgb, uint32_t* raycount, int nthreads) {
+    if (!d || !starts || !ends || n < 0 || depth < 0) return RT_EINVAL;
+    Scene s;
+    int rc = scene_build(d, &s);
+    if (rc) { scene_free(&s); return rc; }
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 256)
+#endif
+    for (int k = 0; k < n; ++k) {
+        Line ray; ray.s = from3(starts + 3 * k); ray.e = from3(ends + 3 * k);
+        P col = pt(0.0, 0.0, 0.0);
+        Count cnt = {0, 0};
+        ray_trace_ray(&s, ray, &col, (unsigned)depth, &cnt);
+        if (rgb) { rgb[3 * k] = col.x; rgb[3 * k + 1] = col.y; rgb[3 * k + 2] = col.z; }
+        if (raycount) raycount[k] = cnt.seg | (cnt.shadow << 16);
+    }
+    scene_free(&s);
+    return RT_OK;
+}
+
+/* g_scene.intersection on arbitrary rays. */
+int oracle_intersect(const rt_scene* d, const double* starts, const double* ends, int n, rt_hit* hits) {
+    if (!d || !starts || !ends || !hits || n < 0) return RT_EINVAL;
+    Scene s;
+    int rc = scene_build(d, &s);
+    if (rc) { scene_free(&s); return rc; }
+    for (int k = 0; k < n; ++k) {
+        Line ray; ray.s = from3(starts + 3 * k); ray.e = from3(ends + 3 * k);
+        Inter in;
+        scene_intersect(&s, ray, &in);
+        rt_hit* h = &hits[k];
+        memset(h, 0, sizeof(*h));
+        h->hit = in.hit;
+        h->material = in.hit ? in.mat_id : -1;
+        if (in.hit) {
+            h->point[0] = in.point.x; h->point[1] = in.point.y; h->point[2] = in.point.z;
+            h->normal[0] = in.normal.x; h->normal[1] = in.normal.y; h->normal[2] = in.normal.z;
+            h->reflected_end[0] = in.refl.e.x; h->reflected_end[1] = in.refl.e.y;
+            h->reflected_end[2] = in.refl.e.z;
+        }
+    }
+    scene_free(&s);
+    return RT_OK;
+}
+
+/* convertStringCoordinate (:1326-1346) for fixture building. */
+void oracle_convert_string_coordinate(const char* sq, double out[3]) {
+    const double edge = 320.0, sqe = 320.0 / 8;
+    P first = pt(-edge / 2, 0.0, edge / 2);
+    P row = pt(0.0, 0.0, -((double)(sq[0] - 'a') + .5) * sqe);
+    P col = pt(((double)(sq[1] - '0' - 1) + .5) * sqe, 0.0, 0.0);
+    P h = pt(0.0, 1.5 * sqe, 0.0);
+    P r = add(add(add(first, row), col), h);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+
+/* FNV-1a 64 over raw bytes (golden-frame hashes). */
+uint64_t oracle_fnv1a64(const void* data, size_t n) {
+    const unsigned char* p = (const unsigned char*)data;
+    uint64_t h = 1469598103934665603ULL;
+    for (size_t i = 0; i < n; ++i) { h ^= p[i]; h *= 1099511628211ULL; }
+    return h;
+}

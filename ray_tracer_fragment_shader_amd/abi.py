@@ -1,0 +1,145 @@
+"""ctypes mirror of include/rt_api.h and the loader for the in-tree librt_amd.so.
+
+The shared library is the product (HIP kernels + C ABI).  There is no Python or CPU fallback: if the
+library is missing, :func:`lib` raises; if no HIP device is present, every render call returns RT_EHIP
+and :func:`check` raises :class:`RtError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_uint8, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "librt_amd.so")
+
+RT_OK = 0
+RT_EINVAL = -1
+RT_EHIP = -2
+RT_ENOMEM = -3
+RT_EUNSUPPORTED = -4
+RT_MAX_SPHERES = 1024
+RT_MAX_LIGHTS = 16
+RT_MAX_DEPTH = 7
+
+D3 = c_double * 3
+
+
+class rt_material(Structure):
+    _fields_ = [("ambient", D3), ("diffuse", D3), ("specular", D3), ("transparency", D3), ("refraction", c_double)]
+
+
+class rt_sphere(Structure):
+    _fields_ = [("center", D3), ("radius", c_double)]
+
+
+class rt_light(Structure):
+    _fields_ = [("color", D3), ("position", D3)]
+
+
+class rt_scene(Structure):
+    _fields_ = [
+        ("position", D3),
+        ("radius", c_double),
+        ("has_board", c_int32),
+        ("n_spheres", c_int32),
+        ("n_lights", c_int32),
+        ("reserved0", c_int32),
+        ("board_position", D3),
+        ("board_half_size", c_double),
+        ("square_edge_size", c_double),
+        ("small_number", c_double),
+        ("attenuation_factor", c_double),
+        ("white_square", rt_material),
+        ("black_square", rt_material),
+        ("sphere_material", rt_material),
+        ("spheres", POINTER(rt_sphere)),
+        ("lights", POINTER(rt_light)),
+    ]
+
+
+class rt_camera(Structure):
+    _fields_ = [("eye", D3), ("look_at", D3), ("up", D3), ("pitch", c_double), ("bottom_x", c_int32),
+                ("bottom_y", c_int32)]
+
+
+class rt_rows(Structure):
+    _fields_ = [("band_height", c_int32), ("n_ranks", c_int32), ("rank", c_int32), ("reserved0", c_int32)]
+
+
+class rt_stats(Structure):
+    _fields_ = [("primary_rays", c_uint64), ("reflect_rays", c_uint64), ("shadow_rays", c_uint64),
+                ("kernel_ms", c_double)]
+
+
+class rt_hit(Structure):
+    _fields_ = [("point", D3), ("normal", D3), ("reflected_end", D3), ("hit", c_int32), ("material", c_int32)]
+
+
+class RtError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str):
+        super().__init__(f"{where}: rt error {code}: {msg}")
+        self.code = code
+
+
+# name -> (restype, argtypes); the exact set declared in include/rt_api.h
+_P = POINTER
+SIGNATURES = {
+    "rt_abi_version": (c_int, []),
+    "rt_last_error": (c_char_p, []),
+    "rt_device_count": (c_int, [_P(c_int)]),
+    "rt_ctx_create": (c_int, [c_int, _P(c_void_p)]),
+    "rt_ctx_destroy": (c_int, [c_void_p]),
+    "rt_scene_init_reference": (c_int, [_P(rt_scene)]),
+    "rt_convert_string_coordinate": (c_int, [c_char_p, _P(c_double)]),
+    "rt_light_position_from_square": (c_int, [c_char_p, _P(c_double)]),
+    "rt_load_scene": (c_int, [_P(c_char_p), _P(c_int32), c_int, _P(rt_scene), _P(rt_sphere), c_int, _P(rt_light)]),
+    "rt_camera_init_reference": (c_int, [_P(rt_camera), c_int, c_int, c_double]),
+    "rt_local_rows": (c_int, [c_int, _P(rt_rows), _P(c_int)]),
+    "rt_global_row": (c_int, [c_int, _P(rt_rows), c_int, _P(c_int)]),
+    "rt_set_scene": (c_int, [c_void_p, _P(rt_scene)]),
+    "rt_render_dev": (c_int, [c_void_p, _P(rt_camera), c_int, c_int, c_int, _P(rt_rows), c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_void_p]),
+    "rt_render": (c_int, [c_void_p, _P(rt_scene), _P(rt_camera), c_int, c_int, c_int, _P(rt_rows), c_void_p,
+                          c_void_p, c_void_p, _P(rt_stats)]),
+    "rt_intersect_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "rt_trace_rays_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "rt_unshuffle_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "rt_write_ppm": (c_int, [c_char_p, _P(c_uint8), c_int, c_int, c_int]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load ray_tracer_fragment_shader_amd/lib/librt_amd.so (built by __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                               f"g.build()'` (make -C ray_tracer_fragment_shader_amd/csrc)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.rt_abi_version() != 1:
+            raise RuntimeError("librt_amd.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    msg = lib().rt_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(code: int, where: str) -> int:
+    if code != RT_OK:
+        raise RtError(code, where, last_error())
+    return code
+
+
+def vec3(v) -> "D3":
+    return D3(*[float(x) for x in v])

@@ -1,0 +1,329 @@
+// rt_host.cpp — host half of the C ABI (include/rt_api.h): scene construction the way the reference
+// app builds g_scene, camera, row banding, device-scene flattening, PPM output.  No HIP calls here.
+//
+// Citations are into /root/reference/Hw4/MySdlApplication.cpp unless a file is named.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "rt_internal.hpp"
+#include "rt_layout.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+// Host mirror of the reference Point (:136-212) with the same operation order.
+struct HP {
+    double x, y, z;
+};
+inline HP hp(double x, double y, double z) { return HP{x, y, z}; }
+inline HP hp(const double* v) { return HP{v[0], v[1], v[2]}; }
+inline HP operator+(HP a, HP b) { return hp(a.x + b.x, a.y + b.y, a.z + b.z); }
+inline HP operator-(HP a, HP b) { return hp(a.x - b.x, a.y - b.y, a.z - b.z); }
+inline HP operator*(double s, HP a) { return hp(s * a.x, s * a.y, s * a.z); }
+inline double dot(HP a, HP b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline HP cross(HP a, HP b) { return hp(a.y * b.z - b.y * a.z, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+inline double length(HP a) { return std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+inline HP normalize(HP a) {
+    double l = length(a);
+    return hp(a.x / l, a.y / l, a.z / l);
+}
+inline void put(double* d, HP a) { d[0] = a.x; d[1] = a.y; d[2] = a.z; }
+
+// Reference constants (:31-52).
+const double kWhite[3] = {1.0, 1.0, 1.0};
+const double kBlack[3] = {0.0, 0.0, 0.0};
+const double kBoardPosition[3] = {0, 0, -160};
+const double kBoardEdge = 320.0;
+const double kBoardHalf = kBoardEdge / 2;
+const unsigned kNumSquares = 8;
+const double kSquareEdge = kBoardEdge / kNumSquares;
+const double kSmall = .0001;
+const double kAttenuation = 100000;
+const double kCamera[3] = {0, 100, 200};
+const double kLookAt[3] = {0, 0, -160};
+const double kUp[3] = {0, 1, 0};
+
+void set_material(rt_material* m, HP a, HP d, HP s, HP t, double r) {
+    put(m->ambient, a);
+    put(m->diffuse, d);
+    put(m->specular, s);
+    put(m->transparency, t);
+    m->refraction = r;
+}
+
+bool valid_square(const char* sq) { return sq && sq[0] != 0 && sq[1] != 0; }
+
+bool all_zero(const double v[3]) { return v[0] == 0 && v[1] == 0 && v[2] == 0; }
+
+}  // namespace
+
+int rt_fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+extern "C" int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+extern "C" const char* rt_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int rt_scene_init_reference(rt_scene* s) {
+    if (!s) return rt_fail(RT_EINVAL, "rt_scene_init_reference: null scene");
+    memset(s, 0, sizeof(*s));
+    put(s->position, hp(kBoardPosition));
+    s->radius = std::sqrt((double)3) * kBoardHalf;                              // :590
+    s->has_board = 1;
+    s->board_half_size = kBoardHalf;
+    s->square_edge_size = kSquareEdge;
+    s->small_number = kSmall;
+    s->attenuation_factor = kAttenuation;
+    HP white = hp(kWhite), black = hp(kBlack);
+    set_material(&s->white_square, .1 * white, .5 * white, white, black, 1);    // :583
+    set_material(&s->black_square, black, .1 * white, black, black, 1);         // :585
+    set_material(&s->sphere_material, black, .1 * white, white, black, 1);      // :586
+    return RT_OK;
+}
+
+extern "C" int rt_convert_string_coordinate(const char* sq, double out[3]) {   // :1326-1346
+    if (!valid_square(sq) || !out) return rt_fail(RT_EINVAL, "rt_convert_string_coordinate: need 2 chars");
+    HP first = hp(-kBoardEdge / 2, 0.0, kBoardEdge / 2);
+    HP row = hp(0.0, 0.0, -(double(sq[0] - 'a') + .5) * kSquareEdge);
+    HP col = hp((double(sq[1] - '0' - 1) + .5) * kSquareEdge, 0.0, 0.0);
+    HP height = hp(0.0, 1.5 * kSquareEdge, 0.0);
+    put(out, first + row + col + height);
+    return RT_OK;
+}
+
+extern "C" int rt_light_position_from_square(const char* sq, double out[3]) {  // :1511
+    double c[3];
+    int rc = rt_convert_string_coordinate(sq, c);
+    if (rc) return rc;
+    put(out, hp(kBoardPosition) + hp(0.0, 3.5 * kSquareEdge, 0.0) + hp(c));
+    return RT_OK;
+}
+
+extern "C" int rt_load_scene(const char* const* squares, const int32_t* types, int n, rt_scene* scene,
+                             rt_sphere* sphere_buf, int sphere_cap, rt_light* light) {
+    if (!scene || n < 0 || (n > 0 && (!squares || !types))) return rt_fail(RT_EINVAL, "rt_load_scene: bad args");
+    std::map<std::string, int> board_map;                                       // boardMap (:595)
+    for (int k = 0; k < n; ++k) {
+        if (!valid_square(squares[k])) return rt_fail(RT_EINVAL, "rt_load_scene: bad square");
+        if (types[k] < 0 || types[k] > 5) return rt_fail(RT_EINVAL, "rt_load_scene: bad object type");
+        board_map[std::string(squares[k])] = types[k];                          // :1467
+    }
+    rt_scene_init_reference(scene);
+    int ns = 0;
+    bool unsupported = false;
+    bool have_light = false;
+    double lpos[3] = {0.0, 0.0, 0.0};                                           // g_lightPosition (:573)
+    for (const auto& kv : board_map) {                                          // :1503-1538
+        const char* sq = kv.first.c_str();
+        switch (kv.second) {
+            case 0:                                                             // LIGHT
+                rt_light_position_from_square(sq, lpos);
+                have_light = true;
+                break;
+            case 3: {                                                           // SPHERE (:1521-1525)
+                if (ns >= sphere_cap || !sphere_buf) return rt_fail(RT_EINVAL, "rt_load_scene: sphere_buf too small");
+                rt_convert_string_coordinate(sq, sphere_buf[ns].center);
+                sphere_buf[ns].radius = kSquareEdge / 2;
+                ++ns;
+                break;
+            }
+            default:                                                            // meshes: outside the GPU path
+                unsupported = true;
+                break;
+        }
+    }
+    (void)have_light;
+    scene->n_spheres = ns;
+    scene->spheres = sphere_buf;
+    if (light) {
+        put(light->color, hp(kWhite));                                          // g_lightColor (:577)
+        put(light->position, hp(lpos));
+        scene->n_lights = 1;                                                    // draw() pushes one light (:1552-1554)
+        scene->lights = light;
+    }
+    if (unsupported)
+        return rt_fail(RT_EUNSUPPORTED, "rt_load_scene: tetrahedron/cube/cylinder/cone are outside the GPU path");
+    return RT_OK;
+}
+
+extern "C" int rt_camera_init_reference(rt_camera* cam, int width, int height, double pitch) {
+    if (!cam || width <= 0 || height <= 0) return rt_fail(RT_EINVAL, "rt_camera_init_reference: bad args");
+    memset(cam, 0, sizeof(*cam));
+    put(cam->eye, hp(kCamera));
+    put(cam->look_at, hp(kLookAt));
+    put(cam->up, hp(kUp));
+    cam->bottom_x = -width / 2;                                                 // :1560
+    cam->bottom_y = -height / 2;
+    cam->pitch = pitch;
+    return RT_OK;
+}
+
+extern "C" int rt_local_rows(int height, const rt_rows* r, int* out) {
+    if (!out || height < 0) return rt_fail(RT_EINVAL, "rt_local_rows: bad args");
+    if (!r || r->n_ranks <= 1) {
+        if (r && (r->n_ranks < 1 || r->rank != 0)) return rt_fail(RT_EINVAL, "rt_local_rows: bad rank");
+        *out = height;
+        return RT_OK;
+    }
+    if (r->band_height <= 0 || r->rank < 0 || r->rank >= r->n_ranks)
+        return rt_fail(RT_EINVAL, "rt_local_rows: bad band geometry");
+    const int hb = r->band_height, G = r->n_ranks;
+    const int full_bands = height / hb, tail = height % hb;
+    int n = (full_bands / G) * hb;
+    int extra_bands = full_bands % G;                                           // bands 0..extra-1 of the last round
+    if (r->rank < extra_bands) n += hb;
+    if (tail && (full_bands % G) == r->rank) n += tail;                         // the partial last band
+    *out = n;
+    return RT_OK;
+}
+
+extern "C" int rt_global_row(int height, const rt_rows* r, int local_row, int* out) {
+    int nl = 0;
+    int rc = rt_local_rows(height, r, &nl);
+    if (rc) return rc;
+    if (!out || local_row < 0 || local_row >= nl) return rt_fail(RT_EINVAL, "rt_global_row: row out of range");
+    if (!r || r->n_ranks <= 1) {
+        *out = local_row;
+        return RT_OK;
+    }
+    const int hb = r->band_height;
+    const int band = local_row / hb, within = local_row % hb;
+    *out = (band * r->n_ranks + r->rank) * hb + within;
+    return RT_OK;
+}
+
+void rt_camera_basis(const rt_camera* cam, double right[3], double upp[3]) {
+    HP ld = hp(cam->look_at) - hp(cam->eye);                                    // :1270
+    HP r = normalize(cross(ld, hp(cam->up)));                                   // :1271-1273
+    HP u = normalize(cross(r, ld));                                             // :1276-1277
+    put(right, r);
+    put(upp, u);
+}
+
+int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
+    if (!s) return rt_fail(RT_EINVAL, "rt_set_scene: null scene");
+    if (s->n_spheres < 0 || s->n_spheres > RT_MAX_SPHERES)
+        return rt_fail(RT_EINVAL, "rt_set_scene: n_spheres out of range [0, " + std::to_string(RT_MAX_SPHERES) + "]");
+    if (s->n_lights < 0 || s->n_lights > RT_MAX_LIGHTS)
+        return rt_fail(RT_EINVAL, "rt_set_scene: n_lights out of range [0, " + std::to_string(RT_MAX_LIGHTS) + "]");
+    if (s->n_spheres > 0 && !s->spheres) return rt_fail(RT_EINVAL, "rt_set_scene: null spheres");
+    if (s->n_lights > 0 && !s->lights) return rt_fail(RT_EINVAL, "rt_set_scene: null lights");
+    if (!(s->small_number >= 0) || !(s->square_edge_size != 0))
+        return rt_fail(RT_EINVAL, "rt_set_scene: bad constants");
+    const rt_material* mats[3] = {&s->white_square, &s->black_square, &s->sphere_material};
+    for (const rt_material* m : mats)
+        if (!all_zero(m->transparency))
+            return rt_fail(RT_EUNSUPPORTED,
+                           "rt_set_scene: transparent materials (transmitted rays) are outside the GPU path");
+
+    const size_t bytes = sizeof(rt::DevScene) + sizeof(rt::DevSphere) * (size_t)s->n_spheres;
+    blob->assign(bytes, 0);
+    rt::DevScene* d = reinterpret_cast<rt::DevScene*>(blob->data());
+    rt::DevSphere* sph = reinterpret_cast<rt::DevSphere*>(d + 1);
+
+    const HP zero = hp(0.0, 0.0, 0.0);
+    const HP bc = hp(s->position) + zero;                                       // g_scene: _position + offset (:739)
+    put(d->bc, bc);
+    d->br2 = s->radius * s->radius;                                             // :750
+    d->bound_on = s->radius > 0;                                                // :747 (g_scene is not _amSphere)
+    d->eps = s->small_number;
+    d->att = s->attenuation_factor;
+    put(d->coff, bc);                                                           // CheckerBoard's positionOffset
+    d->half = s->board_half_size;
+    d->square = s->square_edge_size;
+
+    d->has_board = 0;
+    if (s->has_board) {
+        // CheckerBoard(p) -> _boundingSquare = Quad(p, Material(), P1..P4) (:1064-1069) ->
+        // Triangle(zero, m, P1,P2,P3), Triangle(zero, m, P1,P3,P4) (:840-841).
+        const double h = s->board_half_size;
+        const HP P[4] = {hp(-h, 0, -h), hp(h, 0, -h), hp(h, 0, h), hp(-h, 0, h)};
+        const int idx[2][3] = {{0, 1, 2}, {0, 2, 3}};
+        const HP quad_pos = hp(s->board_position) + bc;                         // Quad: _position + offset
+        const HP tri_pos = zero + quad_pos;                                     // Triangle: zero + offset (:640)
+        bool degenerate[2];
+        for (int t = 0; t < 2; ++t) {
+            HP v0 = P[idx[t][0]], v1 = P[idx[t][1]], v2 = P[idx[t][2]];
+            HP u = v1 - v0, v = v2 - v0;                                        // :413-414
+            HP n = cross(u, v);                                                 // :415
+            degenerate[t] = length(n) < s->small_number;                        // :418
+            n = normalize(n);                                                   // :422
+            double uv = dot(u, v), uu = dot(u, u), vv = dot(v, v);             // :424-426
+            double den = uv * uv - uu * vv;                                     // :428
+            if (std::fabs(den) < s->small_number) degenerate[t] = true;         // :430
+            rt::DevTri& T = d->tri[t];
+            put(T.v0, tri_pos + v0);                                            // :641
+            put(T.u, u);
+            put(T.v, v);
+            put(T.n, n);
+            T.uv = uv;
+            T.uu = uu;
+            T.vv = vv;
+            T.den = den;
+        }
+        // The kernel shares the plane step of the two triangles; the reference board always satisfies
+        // this (same vertex 0, same normal).  A degenerate board never intersects (:633-637).
+        if (!degenerate[0] && !degenerate[1]) {
+            if (memcmp(d->tri[0].v0, d->tri[1].v0, sizeof(d->tri[0].v0)) != 0 ||
+                memcmp(d->tri[0].n, d->tri[1].n, sizeof(d->tri[0].n)) != 0)
+                return rt_fail(RT_EUNSUPPORTED, "rt_set_scene: board triangles do not share a plane");
+            d->has_board = 1;
+        } else if (degenerate[0] != degenerate[1]) {
+            return rt_fail(RT_EUNSUPPORTED, "rt_set_scene: half-degenerate board");
+        }
+    }
+    for (int m = 0; m < 3; ++m) {
+        for (int q = 0; q < 3; ++q) {
+            d->mat[m].amb[q] = mats[m]->ambient[q];
+            d->mat[m].diff[q] = mats[m]->diffuse[q];
+            d->mat[m].spec[q] = mats[m]->specular[q];
+        }
+    }
+    d->n_lights = s->n_lights;
+    for (int k = 0; k < s->n_lights; ++k) {
+        for (int q = 0; q < 3; ++q) {
+            d->light[k].pos[q] = s->lights[k].position[q];
+            d->light[k].col[q] = s->lights[k].color[q];
+        }
+    }
+    d->n_spheres = s->n_spheres;
+    for (int k = 0; k < s->n_spheres; ++k) {
+        put(sph[k].c, hp(s->spheres[k].center) + bc);                          // sphere: _position + offset
+        sph[k].r2 = s->spheres[k].radius * s->spheres[k].radius;                // :750
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_write_ppm(const char* path, const uint8_t* px, int W, int H, int channels) {
+    // writePpmScreenshot (Hw4/ppm.cpp:15-25): header "P6 W H 255\n", then the bottom-up GL image's rows
+    // written top-down (image[3*w*(h-1-i)]).
+    if (!path || !px || W <= 0 || H <= 0 || (channels != 3 && channels != 4))
+        return rt_fail(RT_EINVAL, "rt_write_ppm: bad args");
+    FILE* f = fopen(path, "wb");
+    if (!f) return rt_fail(RT_EINVAL, std::string("rt_write_ppm: cannot open ") + path);
+    fprintf(f, "P6 %d %d 255\n", W, H);
+    std::vector<unsigned char> row((size_t)W * 3);
+    for (int i = 0; i < H; ++i) {
+        const uint8_t* src = px + (size_t)(H - 1 - i) * W * channels;
+        for (int x = 0; x < W; ++x) {
+            row[3 * x] = src[channels * x];
+            row[3 * x + 1] = src[channels * x + 1];
+            row[3 * x + 2] = src[channels * x + 2];
+        }
+        if (fwrite(row.data(), 1, row.size(), f) != row.size()) {
+            fclose(f);
+            return rt_fail(RT_EINVAL, "rt_write_ppm: short write");
+        }
+    }
+    fclose(f);
+    return RT_OK;
+}

@@ -1,0 +1,18 @@
+// rt_internal.hpp — host-side helpers shared by rt_host.cpp and rt_kernel.hip (not part of the ABI).
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+
+// Record `msg` as this thread's rt_last_error() and return `code`.
+int rt_fail(int code, const std::string& msg);
+
+// Validate an rt_scene and flatten it into the device record (rt::DevScene followed by the spheres),
+// precomputing every derived quantity with the reference's operation order.
+int rt_build_dev_scene(const rt_scene* scene, std::vector<unsigned char>* blob);
+
+// rayTraceScreen basis (MySdlApplication.cpp:1270-1277): right = normalize(LD x up),
+// up' = normalize(right x LD), LD = look_at - eye.
+void rt_camera_basis(const rt_camera* cam, double right[3], double upp[3]);

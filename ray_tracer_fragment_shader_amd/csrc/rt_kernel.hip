@@ -1,0 +1,464 @@
+// rt_kernel.hip — MI355X (gfx950) kernels and the device half of the C ABI (include/rt_api.h).
+//
+// Kernels
+//   rt_render_kernel<B, LDS>  one work-item per pixel, FP64, iterative bounce loop (rt_device.hpp).
+//                             Workgroup = 256 work-items = 4 wave64; the workgroup owns a 32 x 8 pixel
+//                             tile and each wave an 8 x 8 sub-tile (square sub-tiles keep a wave's rays
+//                             coherent, so the __any early-out in the bounce loop fires for whole waves).
+//                             The scene (bounding sphere, board, materials, lights, spheres; < 36 KB at
+//                             the 1024-sphere maximum, ~3 KB at 64) is copied into LDS once per
+//                             workgroup (LDS = 1) or read through the scalar cache (LDS = 0).
+//                             Results are staged through LDS and written back as whole 32-pixel rows
+//                             (512 B of RGBA32F per row segment), so framebuffer stores are coalesced.
+//   rt_trace_rays_kernel<B>   rayTraceRay on an arbitrary ray list (parity / fuzz entry point).
+//   rt_intersect_kernel       g_scene.intersection on an arbitrary ray list (primitive KATs).
+//   rt_unshuffle_kernel       multi-GPU: gathered row bands -> image order.
+//
+// Reference: /root/reference/Hw4/MySdlApplication.cpp (rayTraceScreen :1251-1324, rayTraceRay
+// :1184-1249, intersection code :611-823, :1084-1113).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "rt_device.hpp"
+#include "rt_internal.hpp"
+
+using namespace rt;
+
+namespace {
+
+constexpr int kTileW = 32;   // workgroup tile: 32 columns ...
+constexpr int kTileH = 8;    // ... x 8 rows = 256 pixels
+constexpr int kThreads = 256;
+
+struct RenderParams {
+    double eye[3];
+    double look[3];
+    double right[3];
+    double upp[3];
+    double pitch;
+    int32_t bottom_x, bottom_y;
+    int32_t width, height;
+    int32_t local_rows;
+    int32_t band_height, n_ranks, rank;
+    int32_t scene_bytes;
+    int32_t pad;
+};
+
+__device__ __forceinline__ int global_row_of(const RenderParams& P, int lr) {
+    if (P.n_ranks <= 1) return lr;
+    int band = lr / P.band_height, within = lr - band * P.band_height;
+    return (band * P.n_ranks + P.rank) * P.band_height + within;
+}
+
+// Copy the scene record into LDS, 16 B per work-item per step.
+__device__ __forceinline__ void stage_scene(char* dst, const DevScene* __restrict__ src, int bytes) {
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    for (int k = threadIdx.x; k < (bytes >> 4); k += kThreads) d[k] = s[k];
+}
+
+__device__ __forceinline__ unsigned char to_u8(double c) {
+    double v = c < 0.0 ? 0.0 : (c > 1.0 ? 1.0 : c);
+    return (unsigned char)(int)floor(v * 255.0 + 0.5);
+}
+
+template <int B, int LDS>
+__global__ __launch_bounds__(kThreads) void rt_render_kernel(const DevScene* __restrict__ gscene,
+                                                             RenderParams P, float4* __restrict__ out32,
+                                                             uchar4* __restrict__ out8,
+                                                             double* __restrict__ out64,
+                                                             uint32_t* __restrict__ outrc) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const DevScene* S;
+    int stage_off;
+    if (LDS) {
+        stage_scene(smem, gscene, P.scene_bytes);
+        S = reinterpret_cast<const DevScene*>(smem);
+        stage_off = P.scene_bytes;
+    } else {
+        S = gscene;
+        stage_off = 0;
+    }
+    float4* st32 = reinterpret_cast<float4*>(smem + stage_off);                        // [8][32] 4 KB
+    double* st64 = reinterpret_cast<double*>(smem + stage_off + 4096);                  // [8][32][3] 6 KB
+    uint32_t* strc = reinterpret_cast<uint32_t*>(smem + stage_off + 4096 + 6144);       // [8][32] 1 KB
+    uchar4* st8 = reinterpret_cast<uchar4*>(smem + stage_off + 4096 + 6144 + 1024);     // [8][32] 1 KB
+    if (LDS) __syncthreads();
+    const DevSphere* sph = spheres_of(S);
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int cx = wave * 8 + (lane & 7);          // column inside the 32 x 8 tile
+    const int cy = lane >> 3;                      // row inside the tile
+    const int tiles_x = (P.width + kTileW - 1) / kTileW;
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int i = tx * kTileW + cx;
+    const int lr = ty * kTileH + cy;
+    const bool valid = i < P.width && lr < P.local_rows;
+
+    d3 col = mk(0.0, 0.0, 0.0);
+    uint32_t seg = 0, sh = 0;
+    if (valid) {
+        const int j = global_row_of(P, lr);
+        d3 right = ld3(P.right), upp = ld3(P.upp);
+        // Primary ray Line(camera, sp), SURVEY.md Appendix B (basis: rayTraceScreen :1270-1279).
+        d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(i + P.bottom_x), right)),
+                    scl(P.pitch * (double)(j + P.bottom_y), upp));
+        col = trace<B>(S, sph, ld3(P.eye), sp, &seg, &sh);
+    }
+
+    // Stage through LDS, then store whole tile rows.
+    const int slot = cy * kTileW + cx;
+    if (out32) st32[slot] = make_float4((float)col.x, (float)col.y, (float)col.z, 1.0f);
+    if (out64) { st64[3 * slot] = col.x; st64[3 * slot + 1] = col.y; st64[3 * slot + 2] = col.z; }
+    if (outrc) strc[slot] = seg | (sh << 16);
+    if (out8) st8[slot] = make_uchar4(to_u8(col.x), to_u8(col.y), to_u8(col.z), 255);
+    __syncthreads();
+    const int oy = tid >> 5, ox = tid & 31;
+    const int gi = tx * kTileW + ox, glr = ty * kTileH + oy;
+    if (gi < P.width && glr < P.local_rows) {
+        const size_t k = (size_t)glr * P.width + gi;
+        if (out32) out32[k] = st32[tid];
+        if (out64) {
+            out64[3 * k] = st64[3 * tid];
+            out64[3 * k + 1] = st64[3 * tid + 1];
+            out64[3 * k + 2] = st64[3 * tid + 2];
+        }
+        if (outrc) outrc[k] = strc[tid];
+        if (out8) out8[k] = st8[tid];
+    }
+}
+
+template <int B>
+__global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene* __restrict__ S,
+                                                                 const double* __restrict__ starts,
+                                                                 const double* __restrict__ ends, int n,
+                                                                 double* __restrict__ rgb,
+                                                                 uint32_t* __restrict__ rc) {
+    const int k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= n) return;
+    uint32_t seg = 0, sh = 0;
+    d3 c = trace<B>(S, spheres_of(S), ld3(starts + 3 * k), ld3(ends + 3 * k), &seg, &sh);
+    if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
+    if (rc) rc[k] = seg | (sh << 16);
+}
+
+__global__ __launch_bounds__(kThreads) void rt_intersect_kernel(const DevScene* __restrict__ S,
+                                                                const double* __restrict__ starts,
+                                                                const double* __restrict__ ends, int n,
+                                                                rt_hit* __restrict__ hits) {
+    const int k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= n) return;
+    const DevSphere* sph = spheres_of(S);
+    d3 p0 = ld3(starts + 3 * k), p1 = ld3(ends + 3 * k);
+    d3 d = sub(p1, p0);
+    d3 u = divs(d, len(d));
+    d3 p;
+    int kind = closest_hit(S, sph, p0, d, u, &p);
+    rt_hit h;
+    h.hit = kind >= 0;
+    h.material = -1;
+    for (int q = 0; q < 3; ++q) { h.point[q] = 0.0; h.normal[q] = 0.0; h.reflected_end[q] = 0.0; }
+    if (kind >= 0) {
+        d3 n, pe;
+        int mat;
+        surface(S, sph, kind, p, u, &n, &mat, &pe);
+        h.material = mat;
+        h.point[0] = p.x; h.point[1] = p.y; h.point[2] = p.z;
+        h.normal[0] = n.x; h.normal[1] = n.y; h.normal[2] = n.z;
+        h.reflected_end[0] = pe.x; h.reflected_end[1] = pe.y; h.reflected_end[2] = pe.z;
+    }
+    hits[k] = h;
+}
+
+// One workgroup per image row; copies the row from its rank's slab, 4 bytes per work-item step.
+__global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* __restrict__ src,
+                                                                uint32_t* __restrict__ dst, int row_words,
+                                                                int height, int band_height, int n_ranks,
+                                                                int slab_rows) {
+    const int j = blockIdx.x;
+    if (j >= height) return;
+    const int band = j / band_height;
+    const int rank = band % n_ranks;
+    const int lr = (band / n_ranks) * band_height + (j - band * band_height);
+    const uint32_t* s = src + ((size_t)rank * slab_rows + lr) * row_words;
+    uint32_t* d = dst + (size_t)j * row_words;
+    for (int w = threadIdx.x; w < row_words; w += kThreads) d[w] = s[w];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Template dispatch.
+template <int LDS>
+hipError_t launch_render_lds(int depth, dim3 grid, size_t lds, hipStream_t st, const DevScene* s,
+                             const RenderParams& P, float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
+#define RT_CASE(b)                                                                                      \
+    case b:                                                                                             \
+        hipLaunchKernelGGL((rt_render_kernel<b, LDS>), grid, dim3(kThreads), lds, st, s, P, o32, o8,    \
+                           o64, orc);                                                                   \
+        break;
+    switch (depth) {
+        RT_CASE(0) RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7)
+        default: return hipErrorInvalidValue;
+    }
+#undef RT_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_rays(int depth, dim3 grid, hipStream_t st, const DevScene* s, const double* a,
+                             const double* b, int n, double* rgb, uint32_t* rc) {
+#define RT_CASE(k)                                                                                      \
+    case k:                                                                                             \
+        hipLaunchKernelGGL((rt_trace_rays_kernel<k>), grid, dim3(kThreads), 0, st, s, a, b, n, rgb, rc);\
+        break;
+    switch (depth) {
+        RT_CASE(0) RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7)
+        default: return hipErrorInvalidValue;
+    }
+#undef RT_CASE
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI — device half.
+
+struct rt_ctx {
+    int device = 0;
+    DevScene* d_scene = nullptr;
+    size_t scene_cap = 0;
+    int scene_bytes = 0;
+    bool scene_set = false;
+    int use_lds = 1;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+#define RT_HIP(call)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (call);                                                                       \
+        if (e_ != hipSuccess) return rt_fail(RT_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+extern "C" int rt_device_count(int* count) {
+    if (!count) return rt_fail(RT_EINVAL, "rt_device_count: null pointer");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return rt_fail(RT_EHIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    *count = n;
+    return RT_OK;
+}
+
+extern "C" int rt_ctx_create(int device, rt_ctx** out) {
+    if (!out) return rt_fail(RT_EINVAL, "rt_ctx_create: null out");
+    *out = nullptr;
+    int n = 0;
+    int rc = rt_device_count(&n);
+    if (rc) return rc;
+    if (device < 0 || device >= n) return rt_fail(RT_EHIP, "rt_ctx_create: no HIP device " + std::to_string(device));
+    RT_HIP(hipSetDevice(device));
+    rt_ctx* c = new rt_ctx();
+    c->device = device;
+    if (const char* e = getenv("RT_SCENE_IN_LDS")) c->use_lds = atoi(e) != 0;
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        delete c;
+        return rt_fail(RT_EHIP, "rt_ctx_create: hipEventCreate failed");
+    }
+    *out = c;
+    return RT_OK;
+}
+
+extern "C" int rt_ctx_destroy(rt_ctx* c) {
+    if (!c) return RT_OK;
+    (void)hipSetDevice(c->device);
+    if (c->d_scene) (void)hipFree(c->d_scene);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    delete c;
+    return RT_OK;
+}
+
+extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
+    if (!c) return rt_fail(RT_EINVAL, "rt_set_scene: null context");
+    std::vector<unsigned char> blob;
+    int rc = rt_build_dev_scene(scene, &blob);
+    if (rc) return rc;
+    RT_HIP(hipSetDevice(c->device));
+    if (blob.size() > c->scene_cap) {
+        if (c->d_scene) RT_HIP(hipFree(c->d_scene));
+        c->d_scene = nullptr;
+        c->scene_cap = 0;
+        if (hipMalloc(&c->d_scene, blob.size()) != hipSuccess)
+            return rt_fail(RT_ENOMEM, "rt_set_scene: hipMalloc failed");
+        c->scene_cap = blob.size();
+    }
+    RT_HIP(hipMemcpy(c->d_scene, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    c->scene_bytes = (int)blob.size();
+    c->scene_set = true;
+    return RT_OK;
+}
+
+static int render_params(const rt_ctx* c, const rt_camera* cam, int W, int H, int depth, const rt_rows* rows,
+                         RenderParams* P) {
+    if (!c) return rt_fail(RT_EINVAL, "render: null context");
+    if (!c->scene_set) return rt_fail(RT_EINVAL, "render: rt_set_scene has not been called");
+    if (!cam) return rt_fail(RT_EINVAL, "render: null camera");
+    if (W <= 0 || H <= 0 || (long long)W * H > (1LL << 31)) return rt_fail(RT_EINVAL, "render: bad image size");
+    if (depth < 0 || depth > RT_MAX_DEPTH) return rt_fail(RT_EINVAL, "render: depth out of range [0, 7]");
+    int nl = 0;
+    int rc = rt_local_rows(H, rows, &nl);
+    if (rc) return rc;
+    memset(P, 0, sizeof(*P));
+    double right[3], upp[3];
+    rt_camera_basis(cam, right, upp);
+    for (int q = 0; q < 3; ++q) {
+        P->eye[q] = cam->eye[q];
+        P->look[q] = cam->look_at[q];
+        P->right[q] = right[q];
+        P->upp[q] = upp[q];
+    }
+    P->pitch = cam->pitch;
+    P->bottom_x = cam->bottom_x;
+    P->bottom_y = cam->bottom_y;
+    P->width = W;
+    P->height = H;
+    P->local_rows = nl;
+    bool banded = rows && rows->n_ranks > 1;
+    P->band_height = banded ? rows->band_height : H;
+    P->n_ranks = banded ? rows->n_ranks : 1;
+    P->rank = banded ? rows->rank : 0;
+    P->scene_bytes = c->scene_bytes;
+    return RT_OK;
+}
+
+extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int depth, const rt_rows* rows,
+                             float* rgba32f, uint8_t* rgba8, double* rgb64f, uint32_t* raycount, void* stream) {
+    RenderParams P;
+    int rc = render_params(c, cam, W, H, depth, rows, &P);
+    if (rc) return rc;
+    if (P.local_rows == 0) return RT_OK;
+    RT_HIP(hipSetDevice(c->device));
+    const int tiles_x = (W + kTileW - 1) / kTileW;
+    const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
+    dim3 grid((unsigned)(tiles_x * tiles_y));
+    const size_t stage = 4096 + 6144 + 1024 + 1024;
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    if (c->use_lds)
+        e = launch_render_lds<1>(depth, grid, c->scene_bytes + stage, st, c->d_scene, P,
+                                 reinterpret_cast<float4*>(rgba32f), reinterpret_cast<uchar4*>(rgba8), rgb64f,
+                                 raycount);
+    else
+        e = launch_render_lds<0>(depth, grid, stage, st, c->d_scene, P, reinterpret_cast<float4*>(rgba32f),
+                                 reinterpret_cast<uchar4*>(rgba8), rgb64f, raycount);
+    if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_kernel launch: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+extern "C" int rt_render(rt_ctx* c, const rt_scene* scene, const rt_camera* cam, int W, int H, int depth,
+                         const rt_rows* rows, float* rgba32f, uint8_t* rgba8, double* rgb64f, rt_stats* stats) {
+    if (!c) return rt_fail(RT_EINVAL, "rt_render: null context");
+    int rc = rt_set_scene(c, scene);
+    if (rc) return rc;
+    RenderParams P;
+    rc = render_params(c, cam, W, H, depth, rows, &P);
+    if (rc) return rc;
+    const size_t npx = (size_t)P.local_rows * W;
+    float* d32 = nullptr;
+    uint8_t* d8 = nullptr;
+    double* d64 = nullptr;
+    uint32_t* drc = nullptr;
+    auto cleanup = [&]() {
+        if (d32) (void)hipFree(d32);
+        if (d8) (void)hipFree(d8);
+        if (d64) (void)hipFree(d64);
+        if (drc) (void)hipFree(drc);
+    };
+    if ((rgba32f && hipMalloc(&d32, npx * 16) != hipSuccess) || (rgba8 && hipMalloc(&d8, npx * 4) != hipSuccess) ||
+        (rgb64f && hipMalloc(&d64, npx * 24) != hipSuccess) || (stats && hipMalloc(&drc, npx * 4) != hipSuccess)) {
+        cleanup();
+        return rt_fail(RT_ENOMEM, "rt_render: hipMalloc of output buffers failed");
+    }
+    hipError_t e = hipEventRecord(c->ev0, nullptr);
+    if (e == hipSuccess) {
+        rc = rt_render_dev(c, cam, W, H, depth, rows, d32, d8, d64, drc, nullptr);
+        if (rc) { cleanup(); return rc; }
+        e = hipEventRecord(c->ev1, nullptr);
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess && rgba32f) e = hipMemcpy(rgba32f, d32, npx * 16, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && rgba8) e = hipMemcpy(rgba8, d8, npx * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && rgb64f) e = hipMemcpy(rgb64f, d64, npx * 24, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && stats) {
+        std::vector<uint32_t> h(npx);
+        e = hipMemcpy(h.data(), drc, npx * 4, hipMemcpyDeviceToHost);
+        uint64_t seg = 0, sh = 0;
+        for (uint32_t v : h) { seg += v & 0xffffu; sh += v >> 16; }
+        stats->primary_rays = npx;
+        stats->reflect_rays = seg - npx;
+        stats->shadow_rays = sh;
+        float ms = 0.f;
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->ev0, c->ev1);
+        stats->kernel_ms = ms;
+    }
+    cleanup();
+    if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+extern "C" int rt_trace_rays_dev(rt_ctx* c, const double* starts, const double* ends, int n, int depth,
+                                 double* rgb64f, uint32_t* raycount, void* stream) {
+    if (!c || !c->scene_set) return rt_fail(RT_EINVAL, "rt_trace_rays_dev: no context/scene");
+    if (n < 0 || (n > 0 && (!starts || !ends))) return rt_fail(RT_EINVAL, "rt_trace_rays_dev: bad rays");
+    if (depth < 0 || depth > RT_MAX_DEPTH) return rt_fail(RT_EINVAL, "rt_trace_rays_dev: depth out of range");
+    if (n == 0) return RT_OK;
+    RT_HIP(hipSetDevice(c->device));
+    dim3 grid((unsigned)((n + kThreads - 1) / kThreads));
+    hipError_t e = launch_trace_rays(depth, grid, (hipStream_t)stream, c->d_scene, starts, ends, n, rgb64f, raycount);
+    if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_trace_rays_kernel: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+extern "C" int rt_intersect_dev(rt_ctx* c, const double* starts, const double* ends, int n, rt_hit* hits,
+                                void* stream) {
+    if (!c || !c->scene_set) return rt_fail(RT_EINVAL, "rt_intersect_dev: no context/scene");
+    if (n < 0 || (n > 0 && (!starts || !ends || !hits))) return rt_fail(RT_EINVAL, "rt_intersect_dev: bad rays");
+    if (n == 0) return RT_OK;
+    RT_HIP(hipSetDevice(c->device));
+    dim3 grid((unsigned)((n + kThreads - 1) / kThreads));
+    hipLaunchKernelGGL(rt_intersect_kernel, grid, dim3(kThreads), 0, (hipStream_t)stream, c->d_scene, starts, ends,
+                       n, hits);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_intersect_kernel: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+extern "C" int rt_unshuffle_dev(const void* gathered, void* image, int W, int H, int elem_bytes, int band_height,
+                                int n_ranks, int slab_rows, void* stream) {
+    if (!gathered || !image) return rt_fail(RT_EINVAL, "rt_unshuffle_dev: null buffer");
+    if (W <= 0 || H <= 0 || band_height <= 0 || n_ranks <= 0 || slab_rows < 0)
+        return rt_fail(RT_EINVAL, "rt_unshuffle_dev: bad geometry");
+    if (elem_bytes <= 0 || ((long long)W * elem_bytes) % 4 != 0)
+        return rt_fail(RT_EINVAL, "rt_unshuffle_dev: row bytes must be a multiple of 4");
+    rt_rows r = {band_height, n_ranks, 0, 0};
+    for (int q = 0; q < n_ranks; ++q) {
+        int nl = 0;
+        r.rank = q;
+        rt_local_rows(H, &r, &nl);
+        if (nl > slab_rows) return rt_fail(RT_EINVAL, "rt_unshuffle_dev: slab_rows smaller than a rank's rows");
+    }
+    const int row_words = (int)(((long long)W * elem_bytes) / 4);
+    hipLaunchKernelGGL(rt_unshuffle_kernel, dim3((unsigned)H), dim3(kThreads), 0, (hipStream_t)stream,
+                       (const uint32_t*)gathered, (uint32_t*)image, row_words, H, band_height, n_ranks, slab_rows);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_unshuffle_kernel: ") + hipGetErrorString(e));
+    return RT_OK;
+}

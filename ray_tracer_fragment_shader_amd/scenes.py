@@ -1,0 +1,186 @@
+"""Scene descriptors: the reference's g_scene built from the same inputs the app uses, plus the canonical
+benchmark scenes of SURVEY.md Appendix B.
+
+A :class:`Scene` mirrors what ``loadScene`` / ``initScene2`` produce in the reference
+(/root/reference/Hw4/MySdlApplication.cpp:1430-1539): a CheckerBoard inserted first, then spheres in
+order, and the per-frame light list ``draw()`` builds (:1552-1554).  Every coordinate comes from the C
+ABI's host helpers (rt_convert_string_coordinate, rt_light_position_from_square), which restate
+``convertStringCoordinate`` (:1326-1346) with the reference's operation order.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+from . import abi
+
+# Enum of the reference (MySdlApplication.cpp:16).
+LIGHT, TETRAHEDRON, CUBE, SPHERE, CYLINDER, CONE = range(6)
+
+WHITE = (1.0, 1.0, 1.0)
+GREY = (0.5, 0.5, 0.5)
+SQUARES_8 = ("d7", "b2", "f5", "h8", "c4", "e2", "g6", "a5")
+
+
+def convert_string_coordinate(square: str) -> Tuple[float, float, float]:
+    out = (ctypes.c_double * 3)()
+    abi.check(abi.lib().rt_convert_string_coordinate(square.encode(), out), "rt_convert_string_coordinate")
+    return tuple(out)
+
+
+def light_position_from_square(square: str) -> Tuple[float, float, float]:
+    out = (ctypes.c_double * 3)()
+    abi.check(abi.lib().rt_light_position_from_square(square.encode(), out), "rt_light_position_from_square")
+    return tuple(out)
+
+
+@dataclass
+class SphereSpec:
+    square: str
+    radius: float
+    y_offset: float = 0.0     # added as Point(0, y_offset, 0) after convertStringCoordinate
+
+    def center(self) -> Tuple[float, float, float]:
+        x, y, z = convert_string_coordinate(self.square)
+        # Point + Point(0.0, y_offset, 0.0): same additions as the reference operator+ (:196-197)
+        return (x + 0.0, y + self.y_offset, z + 0.0)
+
+
+@dataclass
+class LightSpec:
+    square: Optional[str]          # None: g_lightPosition's default (0,0,0) (:573), as with no light entry
+    color: Tuple[float, float, float] = WHITE
+
+    def position(self) -> Tuple[float, float, float]:
+        if self.square is None:
+            return (0.0, 0.0, 0.0)
+        return light_position_from_square(self.square)
+
+
+@dataclass
+class Scene:
+    """A g_scene: board (first child) + spheres, and the light list of one frame."""
+    spheres: List[SphereSpec] = field(default_factory=list)
+    lights: List[LightSpec] = field(default_factory=list)
+    has_board: bool = True
+    _keep: list = field(default_factory=list, repr=False)
+
+    def to_abi(self) -> abi.rt_scene:
+        L = abi.lib()
+        s = abi.rt_scene()
+        abi.check(L.rt_scene_init_reference(ctypes.byref(s)), "rt_scene_init_reference")
+        s.has_board = 1 if self.has_board else 0
+        ns, nl = len(self.spheres), len(self.lights)
+        sph = (abi.rt_sphere * max(ns, 1))()
+        for k, sp in enumerate(self.spheres):
+            sph[k].center = abi.vec3(sp.center())
+            sph[k].radius = float(sp.radius)
+        lts = (abi.rt_light * max(nl, 1))()
+        for k, lt in enumerate(self.lights):
+            lts[k].color = abi.vec3(lt.color)
+            lts[k].position = abi.vec3(lt.position())
+        s.n_spheres, s.n_lights = ns, nl
+        s.spheres = ctypes.cast(sph, ctypes.POINTER(abi.rt_sphere))
+        s.lights = ctypes.cast(lts, ctypes.POINTER(abi.rt_light))
+        self._keep = [sph, lts]          # keep the arrays alive as long as the Scene
+        return s
+
+    # the reference harness (oracle/_ref) rebuilds the same scene from the reference's own classes
+    def ref_args(self):
+        ns, nl = len(self.spheres), len(self.lights)
+        sq = "".join(sp.square for sp in self.spheres).encode()
+        yoff = (ctypes.c_double * max(ns, 1))(*[sp.y_offset for sp in self.spheres])
+        rad = (ctypes.c_double * max(ns, 1))(*[sp.radius for sp in self.spheres])
+        if any(lt.square is None for lt in self.lights):
+            raise ValueError("the reference harness places lights by square")
+        lsq = "".join(lt.square for lt in self.lights).encode()
+        lcol = (ctypes.c_double * max(3 * nl, 1))(*[c for lt in self.lights for c in lt.color])
+        return (sq, yoff, rad, ns, lsq, lcol, nl)
+
+
+def load_scene(entries: Sequence[Tuple[str, int]]) -> Scene:
+    """loadScene semantics (MySdlApplication.cpp:1495-1539) via the C ABI: later duplicates win, entries
+    are visited in std::map<string> order, the last light wins, one white light.  Mesh types raise
+    RtError(RT_EUNSUPPORTED)."""
+    L = abi.lib()
+    n = len(entries)
+    squares = (ctypes.c_char_p * max(n, 1))(*[e[0].encode() for e in entries])
+    types = (ctypes.c_int32 * max(n, 1))(*[int(e[1]) for e in entries])
+    s = abi.rt_scene()
+    buf = (abi.rt_sphere * max(n, 1))()
+    light = abi.rt_light()
+    abi.check(L.rt_load_scene(squares, types, n, ctypes.byref(s), buf, max(n, 1), ctypes.byref(light)),
+              "rt_load_scene")
+    board = {}
+    for sq, t in entries:
+        board[sq] = t
+    spheres = [SphereSpec(sq, 20.0) for sq in sorted(board) if board[sq] == SPHERE]
+    lights_sq = [sq for sq in sorted(board) if board[sq] == LIGHT]
+    # draw() always pushes one light; with no light entry g_lightPosition keeps its default (0,0,0)
+    scene = Scene(spheres=spheres, lights=[LightSpec(lights_sq[-1] if lights_sq else None)])
+    scene._abi_loaded = (s, buf, light)
+    return scene
+
+
+@dataclass(frozen=True)
+class Config:
+    name: str
+    width: int
+    height: int
+    n_spheres: int
+    n_lights: int
+    depth: int
+    gpus: int = 1
+
+    @property
+    def pitch(self) -> float:
+        return 500.0 / self.width          # canonical framing
+
+    def scene(self) -> Scene:
+        if self.n_spheres == 64:
+            sph = [SphereSpec(chr(ord("a") + r) + chr(ord("1") + c), 10.0, float(((r + c) % 3) * 25))
+                   for r in range(8) for c in range(8)]
+        else:
+            sph = [SphereSpec(sq, 20.0) for sq in SQUARES_8[: self.n_spheres]]
+        lights = [LightSpec("b6", WHITE), LightSpec("g3", GREY)][: self.n_lights]
+        return Scene(spheres=sph, lights=lights)
+
+    def camera(self, width: Optional[int] = None, height: Optional[int] = None) -> abi.rt_camera:
+        """draw()'s camera; for a reduced-resolution render the pitch follows 500/width."""
+        w = width or self.width
+        h = height or self.height
+        return make_camera(w, h, 500.0 / w)
+
+
+def make_camera(width: int, height: int, pitch: float) -> abi.rt_camera:
+    cam = abi.rt_camera()
+    abi.check(abi.lib().rt_camera_init_reference(ctypes.byref(cam), width, height, float(pitch)),
+              "rt_camera_init_reference")
+    return cam
+
+
+# BASELINE.json configs (SURVEY.md §8 shorthand)
+CONFIGS = {
+    "c1": Config("c1", 640, 480, 3, 1, 0),
+    "c2": Config("c2", 1920, 1080, 8, 1, 1),
+    "c3": Config("c3", 3840, 2160, 8, 2, 2),
+    "c4": Config("c4", 3840, 2160, 8, 2, 2, gpus=8),
+    "c5": Config("c5", 7680, 4320, 64, 2, 3, gpus=8),
+}
+
+# Pinned actual-traced ray counts (from the reference's rayTraceRay)
+PINNED_RAYS = {"c1": 380_817, "c2": 3_684_271, "c3": 18_956_255, "c5": 90_722_787}
+
+
+def rows(band_height: int = 1, n_ranks: int = 1, rank: int = 0) -> abi.rt_rows:
+    r = abi.rt_rows()
+    r.band_height, r.n_ranks, r.rank = band_height, n_ranks, rank
+    return r
+
+
+def local_rows(height: int, r: Optional[abi.rt_rows]) -> int:
+    out = ctypes.c_int()
+    abi.check(abi.lib().rt_local_rows(height, ctypes.byref(r) if r is not None else None, ctypes.byref(out)),
+              "rt_local_rows")
+    return out.value

@@ -1,0 +1,140 @@
+"""C ABI (include/rt_api.h) on the CPU: the library loads, exports every declared symbol, and the host-side
+entry points (scene construction, camera, row banding, PPM) behave like the reference.  No GPU compute."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from ray_tracer_fragment_shader_amd import abi, scenes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rt_api.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(rt_[a-z_0-9]+)\s*\(", src, flags=re.M)))
+
+
+def test_every_declared_symbol_is_exported():
+    names = declared_functions()
+    assert len(names) >= 19
+    L = abi.lib()
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(abi.SIGNATURES), set(names) ^ set(abi.SIGNATURES)
+
+
+def test_struct_layouts_match_header_sizes():
+    # sizes implied by include/rt_api.h on LP64
+    assert ctypes.sizeof(abi.rt_material) == 13 * 8
+    assert ctypes.sizeof(abi.rt_sphere) == 32
+    assert ctypes.sizeof(abi.rt_light) == 48
+    assert ctypes.sizeof(abi.rt_camera) == 10 * 8 + 8
+    assert ctypes.sizeof(abi.rt_rows) == 16
+    assert ctypes.sizeof(abi.rt_hit) == 80
+    assert ctypes.sizeof(abi.rt_scene) == 4 * 8 + 16 + 3 * 8 + 4 * 8 + 3 * 13 * 8 + 16
+
+
+def test_no_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    ctx = ctypes.c_void_p()
+    assert abi.lib().rt_ctx_create(0, ctypes.byref(ctx)) == abi.RT_EHIP
+    assert abi.last_error()
+
+
+def test_reference_constants_and_materials():
+    s = abi.rt_scene()
+    abi.check(abi.lib().rt_scene_init_reference(ctypes.byref(s)), "init")
+    assert list(s.position) == [0.0, 0.0, -160.0]
+    assert s.radius == np.sqrt(3.0) * 160.0
+    assert s.board_half_size == 160.0 and s.square_edge_size == 40.0
+    assert s.small_number == 1e-4 and s.attenuation_factor == 1e5
+    assert list(s.white_square.ambient) == [0.1] * 3 and list(s.white_square.diffuse) == [0.5] * 3
+    assert list(s.black_square.diffuse) == [0.1] * 3 and list(s.black_square.specular) == [0.0] * 3
+    assert list(s.sphere_material.specular) == [1.0] * 3 and list(s.sphere_material.ambient) == [0.0] * 3
+
+
+def test_convert_string_coordinate():
+    # "b6" -> (60, 60, 100); light at (60, 200, -60)
+    assert scenes.convert_string_coordinate("b6") == (60.0, 60.0, 100.0)
+    assert scenes.light_position_from_square("b6") == (60.0, 200.0, -60.0)
+    assert scenes.convert_string_coordinate("a1") == (-140.0, 60.0, 140.0)
+    assert scenes.convert_string_coordinate("h8") == (140.0, 60.0, -140.0)
+
+
+@pytest.mark.ref
+def test_convert_string_coordinate_vs_reference():
+    from oracle import pyoracle as po
+    if not po.ref_available():
+        pytest.skip("no reference build here")
+    out = (ctypes.c_double * 3)()
+    for r in "abcdefgh":
+        for c in "12345678":
+            po.ref().ref_convert_string_coordinate((r + c).encode(), out)
+            assert scenes.convert_string_coordinate(r + c) == tuple(out)
+
+
+def test_load_scene_semantics():
+    S, L = scenes.SPHERE, scenes.LIGHT
+    entries = [("d7", S), ("b6", L), ("a1", S), ("d7", S), ("c3", L), ("b2", S), ("b2", L)]
+    sc = scenes.load_scene(entries)
+    s, buf, light = sc._abi_loaded
+    # map order: a1, b2, b6, c3, d7 ; b2 was overwritten by LIGHT -> spheres a1, d7 ; last light c3
+    assert s.n_spheres == 2
+    assert [tuple(buf[k].center) for k in range(2)] == [scenes.convert_string_coordinate("a1"),
+                                                         scenes.convert_string_coordinate("d7")]
+    assert buf[0].radius == 20.0
+    assert tuple(light.position) == scenes.light_position_from_square("c3")
+    assert s.n_lights == 1 and list(light.color) == [1.0, 1.0, 1.0]
+    assert [sp.square for sp in sc.spheres] == ["a1", "d7"]
+    with pytest.raises(abi.RtError) as e:
+        scenes.load_scene([("a1", scenes.CUBE)])
+    assert e.value.code == abi.RT_EUNSUPPORTED
+
+
+def test_camera_reference():
+    cam = scenes.make_camera(641, 481, 1.0)
+    assert list(cam.eye) == [0.0, 100.0, 200.0] and list(cam.look_at) == [0.0, 0.0, -160.0]
+    assert cam.bottom_x == -320 and cam.bottom_y == -240
+
+
+@pytest.mark.parametrize("H,G,hb", [(1080, 8, 8), (1080, 3, 7), (13, 4, 5), (7, 8, 1), (2160, 8, 16), (1, 2, 4)])
+def test_row_bands_partition_exactly(H, G, hb):
+    L = abi.lib()
+    seen = []
+    for r in range(G):
+        rows = scenes.rows(hb, G, r)
+        n = scenes.local_rows(H, rows)
+        g = ctypes.c_int()
+        for lr in range(n):
+            abi.check(L.rt_global_row(H, ctypes.byref(rows), lr, ctypes.byref(g)), "rt_global_row")
+            assert (g.value // hb) % G == r
+            seen.append(g.value)
+    assert sorted(seen) == list(range(H))
+
+
+def test_write_ppm_matches_writePpmScreenshot(tmp_path):
+    W, H = 5, 3
+    img = np.arange(W * H * 4, dtype=np.uint8).reshape(H, W, 4)   # bottom-up, as glReadPixels
+    p = tmp_path / "x.ppm"
+    abi.check(abi.lib().rt_write_ppm(str(p).encode(), img.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), W, H, 4),
+              "rt_write_ppm")
+    data = p.read_bytes()
+    hdr = b"P6 5 3 255\n"
+    assert data.startswith(hdr)
+    body = np.frombuffer(data[len(hdr):], np.uint8).reshape(H, W, 3)
+    assert np.array_equal(body, img[::-1, :, :3])
+
+
+def test_errors_on_bad_host_args():
+    L = abi.lib()
+    assert L.rt_convert_string_coordinate(b"a", (ctypes.c_double * 3)()) == abi.RT_EINVAL
+    assert L.rt_local_rows(10, ctypes.byref(scenes.rows(0, 2, 0)), ctypes.byref(ctypes.c_int())) == abi.RT_EINVAL
+    assert L.rt_local_rows(10, ctypes.byref(scenes.rows(4, 2, 2)), ctypes.byref(ctypes.c_int())) == abi.RT_EINVAL
+    assert L.rt_set_scene(None, None) == abi.RT_EINVAL

@@ -1,0 +1,240 @@
+"""GPU parity: the HIP path (lib/librt_amd.so through the C ABI) against the reference-generated golden
+fixtures and the CPU oracle, on the same inputs.
+
+Tolerance: the north-star bar is L-infinity <= 1e-4 per channel (TOL below).  The kernel keeps the
+reference's FP64 operation order (-ffp-contract=off, IEEE div/sqrt), so these tests also require
+bit-exact equality; a single flipped hit/shadow/checker decision would show up as an error near 1.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import pyoracle as po  # noqa: E402
+from ray_tracer_fragment_shader_amd import abi, scenes  # noqa: E402
+from ray_tracer_fragment_shader_amd.tracer import Tracer, decode_hits, unshuffle  # noqa: E402
+
+from . import golden  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+CAM = np.array([0.0, 100.0, 200.0])
+
+
+@pytest.fixture(scope="module")
+def tr():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a HIP device")
+    t = Tracer(0)
+    yield t
+    t.close()
+
+
+def _render64(tr, scene, cam, W, H, depth, rows=None):
+    tr.set_scene(scene)
+    b = tr.render(cam, W, H, depth, rows=rows, rgba32f=False, rgb64f=True, raycount=True)
+    torch.cuda.synchronize()
+    return b["rgb64f"].cpu().numpy(), b["raycount"].cpu().numpy().view(np.uint32)
+
+
+def _assert_parity(got, want):
+    err = np.abs(got - want).max() if got.size else 0.0
+    assert err <= TOL, f"L-inf {err}"
+    assert np.array_equal(got, want), f"not bit-exact: {(got != want).any(axis=-1).sum()} pixels differ"
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c5"])
+def test_small_frame_vs_reference(tr, name):
+    cfg = scenes.CONFIGS[name]
+    g = golden.frames(name)
+    W, H = (int(x) for x in g["small_wh"])
+    rgb, _ = _render64(tr, cfg.scene(), cfg.camera(W, H), W, H, cfg.depth)
+    _assert_parity(rgb, g["small"])
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c5"])
+def test_sampled_full_res_pixels_vs_reference(tr, name):
+    cfg = scenes.CONFIGS[name]
+    g = golden.frames(name)
+    tr.set_scene(cfg.scene())
+    sp = po.screen_points(cfg.camera(), cfg.width, cfg.height)[g["pj"], g["pi"]]
+    starts = torch.tensor(np.tile(CAM, (len(sp), 1)), device="cuda")
+    ends = torch.tensor(np.ascontiguousarray(sp), device="cuda")
+    rgb, _ = tr.trace_rays(starts, ends, cfg.depth)
+    _assert_parity(rgb.cpu().numpy(), g["samples"])
+
+
+@pytest.mark.parametrize("name", ["c1", "c2"])
+def test_full_frame_vs_oracle(tr, name):
+    cfg = scenes.CONFIGS[name]
+    sc = cfg.scene()
+    rgb, rc = _render64(tr, sc, cfg.camera(), cfg.width, cfg.height, cfg.depth)
+    want, want_rc = po.render(sc.to_abi(), cfg.camera(), cfg.width, cfg.height, cfg.depth)
+    _assert_parity(rgb, want)
+    assert np.array_equal(rc, want_rc)
+    assert int((rc & 0xFFFF).sum()) + int((rc >> 16).sum()) == scenes.PINNED_RAYS[name]
+
+
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_full_frame_hash_vs_reference(tr, name):
+    """Full-size frames: size-independent checks — FNV-1a of the whole float64 frame equals the hash of
+    the reference's own frame, and the traced-ray total equals the reference's."""
+    cfg = scenes.CONFIGS[name]
+    rgb, rc = _render64(tr, cfg.scene(), cfg.camera(), cfg.width, cfg.height, cfg.depth)
+    assert f"{po.fnv1a64(rgb):016x}" == golden.manifest()["frames"][name]["fnv1a64"]
+    assert int((rc & 0xFFFF).sum()) + int((rc >> 16).sum()) == scenes.PINNED_RAYS[name]
+
+
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_intersection_kat(tr, name):
+    cfg = scenes.CONFIGS[name]
+    k = golden.kat(name)
+    tr.set_scene(cfg.scene())
+    raw = tr.intersect(torch.tensor(k["starts"], device="cuda"), torch.tensor(k["ends"], device="cuda"))
+    got = decode_hits(raw)
+    assert np.array_equal(got["hit"], k["hit"])
+    assert np.array_equal(got["material"], k["material"])
+    for f in ("point", "normal", "reflected_end"):
+        assert np.array_equal(got[f], k[f]), f
+
+
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_trace_rays_kat(tr, name):
+    cfg = scenes.CONFIGS[name]
+    k = golden.kat(name)
+    tr.set_scene(cfg.scene())
+    s = torch.tensor(k["starts"], device="cuda")
+    e = torch.tensor(k["ends"], device="cuda")
+    for depth in range(4):
+        rgb, _ = tr.trace_rays(s, e, depth)
+        _assert_parity(rgb.cpu().numpy(), k["colors"][depth])
+
+
+def test_output_formats_consistent(tr):
+    cfg = scenes.CONFIGS["c2"]
+    W, H = 321, 203
+    tr.set_scene(cfg.scene())
+    b = tr.render(cfg.camera(W, H), W, H, cfg.depth, rgba32f=True, rgba8=True, rgb64f=True, raycount=True)
+    torch.cuda.synchronize()
+    c64 = b["rgb64f"].cpu().numpy()
+    c32 = b["rgba32f"].cpu().numpy()
+    c8 = b["rgba8"].cpu().numpy()
+    assert np.array_equal(c32[..., :3], c64.astype(np.float32))
+    assert np.all(c32[..., 3] == 1.0)
+    want8 = np.floor(np.clip(c64, 0.0, 1.0) * 255.0 + 0.5).astype(np.uint8)
+    assert np.array_equal(c8[..., :3], want8)
+    assert np.all(c8[..., 3] == 255)
+
+
+def test_scene_in_lds_and_scalar_cache_agree():
+    cfg = scenes.CONFIGS["c5"]
+    W, H = 200, 150
+    out = []
+    for mode in ("1", "0"):
+        os.environ["RT_SCENE_IN_LDS"] = mode
+        t = Tracer(0)
+        out.append(_render64(t, cfg.scene(), cfg.camera(W, H), W, H, cfg.depth)[0])
+        t.close()
+    os.environ.pop("RT_SCENE_IN_LDS")
+    assert np.array_equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("G,hb", [(2, 8), (3, 5), (8, 16), (4, 1)])
+def test_row_bands_and_unshuffle(tr, G, hb):
+    cfg = scenes.CONFIGS["c2"]
+    W, H = 250, 133
+    full, _ = _render64(tr, cfg.scene(), cfg.camera(W, H), W, H, cfg.depth)
+    slab = max(scenes.local_rows(H, scenes.rows(hb, G, r)) for r in range(G))
+    gathered = torch.zeros((G, slab, W, 3), dtype=torch.float64, device="cuda")
+    for r in range(G):
+        part, _ = _render64(tr, cfg.scene(), cfg.camera(W, H), W, H, cfg.depth, rows=scenes.rows(hb, G, r))
+        gathered[r, : part.shape[0]] = torch.tensor(part, device="cuda")
+    img = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
+    unshuffle(gathered, img, W, H, hb, G, slab)
+    torch.cuda.synchronize()
+    assert np.array_equal(img.cpu().numpy(), full)
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (33, 17), (31, 9), (64, 8), (7, 300)])
+@pytest.mark.parametrize("depth", [0, 3, 7])
+def test_odd_sizes_and_depths(tr, W, H, depth):
+    cfg = scenes.CONFIGS["c3"]
+    sc = cfg.scene()
+    rgb, rc = _render64(tr, sc, cfg.camera(W, H), W, H, depth)
+    want, want_rc = po.render(sc.to_abi(), cfg.camera(W, H), W, H, depth)
+    _assert_parity(rgb, want)
+    assert np.array_equal(rc, want_rc)
+
+
+def _random_scene(rng, n_spheres, n_lights, board=True):
+    sq = [chr(ord("a") + int(rng.integers(0, 8))) + chr(ord("1") + int(rng.integers(0, 8)))
+          for _ in range(n_spheres)]
+    sph = [scenes.SphereSpec(s, float(rng.uniform(2, 45)), float(rng.uniform(-70, 90))) for s in sq]
+    lts = [scenes.LightSpec(chr(ord("a") + int(rng.integers(0, 8))) + chr(ord("1") + int(rng.integers(0, 8))),
+                            tuple(float(x) for x in rng.uniform(0, 1, 3))) for _ in range(n_lights)]
+    return scenes.Scene(spheres=sph, lights=lts, has_board=board)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_random_scenes_vs_oracle(tr, seed):
+    rng = np.random.default_rng(seed)
+    sc = _random_scene(rng, int(rng.integers(0, 40)), int(rng.integers(0, 5)), board=bool(seed % 3))
+    W, H = 160, 120
+    cam = scenes.make_camera(W, H, float(rng.uniform(0.5, 4.0)))
+    depth = int(rng.integers(0, 8))
+    rgb, rc = _render64(tr, sc, cam, W, H, depth)
+    want, want_rc = po.render(sc.to_abi(), cam, W, H, depth)
+    _assert_parity(rgb, want)
+    assert np.array_equal(rc, want_rc)
+    # random rays from random origins through the same scene
+    s = rng.uniform(-300, 300, (4096, 3))
+    e = s + rng.normal(size=(4096, 3)) * rng.uniform(0.1, 100, (4096, 1))
+    g, _ = tr.trace_rays(torch.tensor(s, device="cuda"), torch.tensor(e, device="cuda"), depth)
+    w, _ = po.trace_rays(sc.to_abi(), s, e, depth)
+    _assert_parity(g.cpu().numpy(), w)
+
+
+def test_max_spheres_and_empty_scene(tr):
+    rng = np.random.default_rng(7)
+    big = _random_scene(rng, abi.RT_MAX_SPHERES, 2)
+    W, H = 64, 48
+    cam = scenes.make_camera(W, H, 500.0 / W)
+    rgb, _ = _render64(tr, big, cam, W, H, 2)
+    want, _ = po.render(big.to_abi(), cam, W, H, 2)
+    _assert_parity(rgb, want)
+    empty = scenes.Scene(spheres=[], lights=[], has_board=False)
+    rgb, rc = _render64(tr, empty, cam, W, H, 3)
+    assert not rgb.any()
+    assert np.all(rc == 1)
+
+
+def test_errors_are_loud(tr):
+    L = abi.lib()
+    cfg = scenes.CONFIGS["c1"]
+    sc = cfg.scene()
+    s = sc.to_abi()
+    s.sphere_material.transparency[0] = 1.0
+    assert L.rt_set_scene(tr._ctx, ctypes.byref(s)) == abi.RT_EUNSUPPORTED
+    s = sc.to_abi()
+    s.n_spheres = abi.RT_MAX_SPHERES + 1
+    assert L.rt_set_scene(tr._ctx, ctypes.byref(s)) == abi.RT_EINVAL
+    tr.set_scene(sc)
+    cam = cfg.camera(8, 8)
+    assert L.rt_render_dev(tr._ctx, ctypes.byref(cam), 8, 8, 8, None, None, None, None, None, None) == abi.RT_EINVAL
+    assert L.rt_render_dev(tr._ctx, ctypes.byref(cam), 0, 8, 1, None, None, None, None, None, None) == abi.RT_EINVAL
+    assert "depth" in abi.last_error() or "size" in abi.last_error()
+
+
+def test_host_buffer_render_and_stats(tr):
+    cfg = scenes.CONFIGS["c2"]
+    sc = cfg.scene()
+    rgb, st = tr.render_host(sc.to_abi(), cfg.camera(), cfg.width, cfg.height, cfg.depth)
+    want, _ = po.render(sc.to_abi(), cfg.camera(), cfg.width, cfg.height, cfg.depth)
+    _assert_parity(rgb, want)
+    assert st.primary_rays + st.reflect_rays + st.shadow_rays == scenes.PINNED_RAYS["c2"]
+    assert st.primary_rays == cfg.width * cfg.height
+    assert st.kernel_ms > 0
