@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <string>
 #include <vector>
@@ -225,16 +226,19 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
             return rt_fail(RT_EUNSUPPORTED,
                            "rt_set_scene: transparent materials (transmitted rays) are outside the GPU path");
 
-    const size_t bytes = sizeof(rt::DevScene) + sizeof(rt::DevSphere) * (size_t)s->n_spheres;
+    const size_t bytes = (size_t)rt::scene_bytes_for(s->n_spheres);
     blob->assign(bytes, 0);
     rt::DevScene* d = reinterpret_cast<rt::DevScene*>(blob->data());
     rt::DevSphere* sph = reinterpret_cast<rt::DevSphere*>(d + 1);
+    rt::DevSphereF* sphf = reinterpret_cast<rt::DevSphereF*>(sph + s->n_spheres);
 
     const HP zero = hp(0.0, 0.0, 0.0);
     const HP bc = hp(s->position) + zero;                                       // g_scene: _position + offset (:739)
     put(d->bc, bc);
     d->br2 = s->radius * s->radius;                                             // :750
     d->bound_on = s->radius > 0;                                                // :747 (g_scene is not _amSphere)
+    // origins with |o - bc|^2 < (R-1)^2 provably pass the cull (proof at rt_device.hpp bound_pass_dp)
+    d->inner2 = s->radius > 2 ? (s->radius - 1) * (s->radius - 1) : -1.0;
     d->eps = s->small_number;
     d->att = s->attenuation_factor;
     put(d->coff, bc);                                                           // CheckerBoard's positionOffset
@@ -269,6 +273,10 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
             T.uu = uu;
             T.vv = vv;
             T.den = den;
+            // den < 0: A > |den| 2^-1070 proves A/den < 0 (nonzero), so the kernel may skip the division.
+            // Otherwise disable the shortcut.
+            T.thr = (den < 0 && std::fabs(den) >= 1024.0) ? std::ldexp(std::fabs(den), -1070)
+                                                          : std::numeric_limits<double>::infinity();
         }
         // The kernel shares the plane step of the two triangles; the reference board always satisfies
         // this (same vertex 0, same normal).  A degenerate board never intersects (:633-637).
@@ -297,8 +305,21 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     }
     d->n_spheres = s->n_spheres;
     for (int k = 0; k < s->n_spheres; ++k) {
-        put(sph[k].c, hp(s->spheres[k].center) + bc);                          // sphere: _position + offset
+        HP c = hp(s->spheres[k].center) + bc;                                   // sphere: _position + offset
+        put(sph[k].c, c);
         sph[k].r2 = s->spheres[k].radius * s->spheres[k].radius;                // :750
+        // FP32 filter image (rt_device.hpp sphere_reject32): centre relative to bc, and
+        // rm = r2 + 4K sC^2 + K r2 rounded up, sC = max|c_i - bc_i|.
+        HP rel = c - bc;
+        double sC = std::max(std::fabs(rel.x), std::max(std::fabs(rel.y), std::fabs(rel.z)));
+        double K = (double)rt::kFilterK;
+        double rm = sph[k].r2 + 4 * K * sC * sC + K * sph[k].r2;
+        sphf[k].cx = (float)rel.x;
+        sphf[k].cy = (float)rel.y;
+        sphf[k].cz = (float)rel.z;
+        float rmf = (float)rm;
+        if ((double)rmf < rm) rmf = std::nextafter(rmf, std::numeric_limits<float>::infinity());
+        sphf[k].rm = rmf;
     }
     return RT_OK;
 }

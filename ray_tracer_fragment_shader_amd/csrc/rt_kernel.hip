@@ -47,7 +47,7 @@ struct RenderParams {
     int32_t local_rows;
     int32_t band_height, n_ranks, rank;
     int32_t scene_bytes;
-    int32_t pad;
+    int32_t n_spheres;
 };
 
 __device__ __forceinline__ int global_row_of(const RenderParams& P, int lr) {
@@ -75,24 +75,52 @@ __global__ __launch_bounds__(kThreads) void rt_render_kernel(const DevScene* __r
                                                              double* __restrict__ out64,
                                                              uint32_t* __restrict__ outrc) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const DevScene* S;
-    int stage_off;
+    const int tid = threadIdx.x;
+    const int ns = P.n_spheres;
+    // LDS: [scene record (LDS = 1)] [DevSpherePrim[ns] | DevSpherePrimF[ns]] [output staging 12 KB]
+    int off = 0;
+    const DevScene* S = gscene;
     if (LDS) {
         stage_scene(smem, gscene, P.scene_bytes);
         S = reinterpret_cast<const DevScene*>(smem);
-        stage_off = P.scene_bytes;
-    } else {
-        S = gscene;
-        stage_off = 0;
+        off = P.scene_bytes;
     }
-    float4* st32 = reinterpret_cast<float4*>(smem + stage_off);                        // [8][32] 4 KB
-    double* st64 = reinterpret_cast<double*>(smem + stage_off + 4096);                  // [8][32][3] 6 KB
-    uint32_t* strc = reinterpret_cast<uint32_t*>(smem + stage_off + 4096 + 6144);       // [8][32] 1 KB
-    uchar4* st8 = reinterpret_cast<uchar4*>(smem + stage_off + 4096 + 6144 + 1024);     // [8][32] 1 KB
-    if (LDS) __syncthreads();
-    const DevSphere* sph = spheres_of(S);
+    DevSpherePrim* prim = reinterpret_cast<DevSpherePrim*>(smem + off);
+    DevSpherePrimF* primf = reinterpret_cast<DevSpherePrimF*>(prim + ns);
+    off += prim_bytes_for(ns);
+    float4* st32 = reinterpret_cast<float4*>(smem + off);                              // [8][32] 4 KB
+    double* st64 = reinterpret_cast<double*>(smem + off + 4096);                        // [8][32][3] 6 KB
+    uint32_t* strc = reinterpret_cast<uint32_t*>(smem + off + 4096 + 6144);             // [8][32] 1 KB
+    uchar4* st8 = reinterpret_cast<uchar4*>(smem + off + 4096 + 6144 + 1024);           // [8][32] 1 KB
 
-    const int tid = threadIdx.x;
+    // Primary-ray sphere data for this frame's camera, once per workgroup: deltaP = C - eye and
+    // dot(deltaP, deltaP) exactly as Shape::intersection computes them for p0 = camera (:740, :750), and
+    // the FP32 filter image f32(deltaP), c0 = r2 - dd + K (S0^2 + r2) rounded up, S0 = max|deltaP_i|.
+    // Filter error < 35 eps32 S0^2 + 2 eps32 r2 << K (S0^2 + r2), K = 256 eps32.
+    const d3 eye = ld3(P.eye);
+    {
+        const DevSphere* gsph = reinterpret_cast<const DevSphere*>(gscene + 1);
+        for (int k = tid; k < ns; k += kThreads) {
+            d3 dP = sub(ld3(gsph[k].c), eye);
+            double dd = dot(dP, dP);
+            DevSpherePrim pp;
+            pp.dP[0] = dP.x; pp.dP[1] = dP.y; pp.dP[2] = dP.z;
+            pp.dd = dd;
+            prim[k] = pp;
+            double s0 = fmax(fabs(dP.x), fmax(fabs(dP.y), fabs(dP.z)));
+            double r2 = gsph[k].r2;
+            double c0 = (r2 - dd) + (double)kFilterK * (s0 * s0 + r2);
+            DevSpherePrimF f;
+            f.dx = (float)dP.x; f.dy = (float)dP.y; f.dz = (float)dP.z;
+            f.c0 = __double2float_ru(c0);
+            primf[k] = f;
+        }
+    }
+    __syncthreads();
+    SceneView V = view_of(S);
+    V.prim = prim;
+    V.primf = primf;
+
     const int wave = tid >> 6, lane = tid & 63;
     const int cx = wave * 8 + (lane & 7);          // column inside the 32 x 8 tile
     const int cy = lane >> 3;                      // row inside the tile
@@ -110,7 +138,8 @@ __global__ __launch_bounds__(kThreads) void rt_render_kernel(const DevScene* __r
         // Primary ray Line(camera, sp), SURVEY.md Appendix B (basis: rayTraceScreen :1270-1279).
         d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(i + P.bottom_x), right)),
                     scl(P.pitch * (double)(j + P.bottom_y), upp));
-        col = trace<B>(S, sph, ld3(P.eye), sp, &seg, &sh);
+        d3 bdP = sub(ld3(V.S->bc), eye);           // bounding-sphere deltaP for p0 = camera
+        col = trace<B, true>(V, eye, sp, bdP, dot(bdP, bdP), &seg, &sh);
     }
 
     // Stage through LDS, then store whole tile rows.
@@ -144,7 +173,7 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
     const int k = blockIdx.x * kThreads + threadIdx.x;
     if (k >= n) return;
     uint32_t seg = 0, sh = 0;
-    d3 c = trace<B>(S, spheres_of(S), ld3(starts + 3 * k), ld3(ends + 3 * k), &seg, &sh);
+    d3 c = trace<B, false>(view_of(S), ld3(starts + 3 * k), ld3(ends + 3 * k), mk(0.0, 0.0, 0.0), 0.0, &seg, &sh);
     if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
     if (rc) rc[k] = seg | (sh << 16);
 }
@@ -155,12 +184,14 @@ __global__ __launch_bounds__(kThreads) void rt_intersect_kernel(const DevScene* 
                                                                 rt_hit* __restrict__ hits) {
     const int k = blockIdx.x * kThreads + threadIdx.x;
     if (k >= n) return;
-    const DevSphere* sph = spheres_of(S);
-    d3 p0 = ld3(starts + 3 * k), p1 = ld3(ends + 3 * k);
-    d3 d = sub(p1, p0);
-    d3 u = divs(d, len(d));
+    const SceneView V = view_of(S);
+    Ray r;
+    r.p0 = ld3(starts + 3 * k);
+    d3 d = sub(ld3(ends + 3 * k), r.p0);
+    set_dir(&r, d, divs(d, len(d)));
+    set_origin_f32(S, &r);
     d3 p;
-    int kind = closest_hit(S, sph, p0, d, u, &p);
+    int kind = closest_hit(V, r, &p);
     rt_hit h;
     h.hit = kind >= 0;
     h.material = -1;
@@ -168,7 +199,7 @@ __global__ __launch_bounds__(kThreads) void rt_intersect_kernel(const DevScene* 
     if (kind >= 0) {
         d3 n, pe;
         int mat;
-        surface(S, sph, kind, p, u, &n, &mat, &pe);
+        surface(V, kind, p, r.u, &n, &mat, &pe);
         h.material = mat;
         h.point[0] = p.x; h.point[1] = p.y; h.point[2] = p.z;
         h.normal[0] = n.x; h.normal[1] = n.y; h.normal[2] = n.z;
@@ -199,6 +230,11 @@ hipError_t launch_render_lds(int depth, dim3 grid, size_t lds, hipStream_t st, c
                              const RenderParams& P, float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
 #define RT_CASE(b)                                                                                      \
     case b:                                                                                             \
+        if (lds > 65536) {                                                                              \
+            hipError_t e_ = hipFuncSetAttribute((const void*)rt_render_kernel<b, LDS>,                  \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);  \
+            if (e_ != hipSuccess) return e_;                                                            \
+        }                                                                                               \
         hipLaunchKernelGGL((rt_render_kernel<b, LDS>), grid, dim3(kThreads), lds, st, s, P, o32, o8,    \
                            o64, orc);                                                                   \
         break;
@@ -234,6 +270,7 @@ struct rt_ctx {
     DevScene* d_scene = nullptr;
     size_t scene_cap = 0;
     int scene_bytes = 0;
+    int n_spheres = 0;
     bool scene_set = false;
     int use_lds = 1;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -302,6 +339,7 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     }
     RT_HIP(hipMemcpy(c->d_scene, blob.data(), blob.size(), hipMemcpyHostToDevice));
     c->scene_bytes = (int)blob.size();
+    c->n_spheres = reinterpret_cast<const rt::DevScene*>(blob.data())->n_spheres;
     c->scene_set = true;
     return RT_OK;
 }
@@ -336,6 +374,7 @@ static int render_params(const rt_ctx* c, const rt_camera* cam, int W, int H, in
     P->n_ranks = banded ? rows->n_ranks : 1;
     P->rank = banded ? rows->rank : 0;
     P->scene_bytes = c->scene_bytes;
+    P->n_spheres = c->n_spheres;
     return RT_OK;
 }
 
@@ -349,7 +388,7 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     const int tiles_x = (W + kTileW - 1) / kTileW;
     const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
     dim3 grid((unsigned)(tiles_x * tiles_y));
-    const size_t stage = 4096 + 6144 + 1024 + 1024;
+    const size_t stage = (size_t)prim_bytes_for(c->n_spheres) + 4096 + 6144 + 1024 + 1024;
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     if (c->use_lds)

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Interleaved in-process timing of rt_render_dev across configs and scene-placement modes
+(RT_SCENE_IN_LDS = 1 / 0).  Prints one JSON line per (config, mode) with median / min kernel ms."""
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from ray_tracer_fragment_shader_amd import scenes  # noqa: E402
+from ray_tracer_fragment_shader_amd.tracer import Tracer  # noqa: E402
+
+
+def main():
+    cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c1", "c2", "c3", "c5"]
+    modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "0"]
+    rounds = int(os.environ.get("ROUNDS", "5"))
+    reps = int(os.environ.get("REPS", "10"))
+    tracers = {}
+    for m in modes:
+        os.environ["RT_SCENE_IN_LDS"] = m
+        tracers[m] = Tracer(0)
+    res = {(c, m): [] for c in cfgs for m in modes}
+    bufs = {}
+    for c in cfgs:
+        cfg = scenes.CONFIGS[c]
+        bufs[c] = tracers[modes[0]].alloc(cfg.width, cfg.height, rgba32f=True, rgba8=True)
+    for _ in range(rounds):
+        for c in cfgs:
+            cfg = scenes.CONFIGS[c]
+            cam = cfg.camera()
+            for m in modes:
+                t = tracers[m]
+                t.set_scene(cfg.scene())
+                t.render_into(cam, cfg.width, cfg.height, cfg.depth, bufs[c])   # warm
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    t.render_into(cam, cfg.width, cfg.height, cfg.depth, bufs[c])
+                e1.record()
+                torch.cuda.synchronize()
+                res[(c, m)].append(e0.elapsed_time(e1) / reps)
+    for (c, m), v in res.items():
+        rays = scenes.PINNED_RAYS[c]
+        med = statistics.median(v)
+        print(json.dumps({"config": c, "lds": m, "median_ms": round(med, 4), "min_ms": round(min(v), 4),
+                          "Mray/s": round(rays / med / 1e3, 1)}))
+
+
+if __name__ == "__main__":
+    main()
