@@ -1,0 +1,180 @@
+// rt_cli.cpp — `rt_render`: the reference application's frame flow on the MI355X path.
+//
+// Reference flow (Hw4/MySdlApplication.cpp): onInit -> initScene2 (stdin dialogue, :1430-1493) ->
+// loadScene (:1495-1539) -> every frame draw() (:1541-1563) -> rayTraceScreen -> GL points; a screenshot
+// would go through writePpmScreenshot (Hw4/ppm.cpp:15-25).  Here: the same dialogue (or a canonical
+// scene) -> rt_load_scene -> rt_render (one HIP launch) -> RGBA8 -> rt_write_ppm.  No SDL/GL window:
+// the image goes to a PPM file (the output path the reference already has).
+//
+//   rt_render --config c2 --out c2.ppm            canonical scene
+//   rt_render --stdin --width 500 --height 500 --pitch 1 --out app.ppm < answers.txt
+//                                                  initScene2's questions answered on stdin
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+
+namespace {
+
+struct Options {
+    std::string config = "c2";
+    std::string out = "frame.ppm";
+    bool from_stdin = false;
+    int width = 0, height = 0, depth = -1, device = 0;
+    double pitch = 0;
+};
+
+[[noreturn]] void die(const std::string& what, int code) {
+    std::fprintf(stderr, "rt_render: %s failed (%d): %s\n", what.c_str(), code, rt_last_error());
+    std::exit(1);
+}
+
+void check(int code, const char* what) {
+    if (code != RT_OK) die(what, code);
+}
+
+// initScene2 (:1430-1493): "(a) light, (b) tetrahedron, (c) cube, (d) sphere, (e) cylinder, (f) cone",
+// then a square "a1-h8", then "yes/no" for another object.  Returns the boardMap entries in input order.
+void read_dialogue(std::vector<std::string>* squares, std::vector<int32_t>* types) {
+    std::string tmp;
+    bool finished = false;
+    while (!finished) {
+        bool answered = false;
+        while (!answered) {
+            std::cout << "Please select the type of object to add:\n"
+                      << "(a) light, (b) tetrahedron, (c) cube, (d) sphere, (e) cylinder, (f) cone" << std::endl;
+            if (!(std::cin >> tmp)) return;
+            answered = tmp.size() <= 1;
+            int type = tmp[0] - 'a';
+            if (type >= 0 && type < 6) {
+                std::cout << "Please enter the position: (a1-h8)" << std::endl;
+                if (!(std::cin >> tmp)) return;
+                squares->push_back(tmp);
+                types->push_back(type);
+            } else {
+                answered = false;
+            }
+        }
+        answered = false;
+        while (!answered) {
+            std::cout << "Would you like to add another object? (yes/no)" << std::endl;
+            if (!(std::cin >> tmp)) return;
+            if (tmp == "no" || tmp == "n") finished = answered = true;
+            else if (tmp == "yes" || tmp == "y") answered = true;
+        }
+    }
+}
+
+struct Canonical {
+    int w, h, nsph, nl, depth;
+};
+
+Canonical canonical(const std::string& c) {
+    if (c == "c1") return {640, 480, 3, 1, 0};
+    if (c == "c2") return {1920, 1080, 8, 1, 1};
+    if (c == "c3" || c == "c4") return {3840, 2160, 8, 2, 2};
+    if (c == "c5") return {7680, 4320, 64, 2, 3};
+    std::fprintf(stderr, "rt_render: unknown config %s\n", c.c_str());
+    std::exit(2);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Options o;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&]() -> std::string {
+            if (i + 1 >= argc) { std::fprintf(stderr, "missing value for %s\n", a.c_str()); std::exit(2); }
+            return argv[++i];
+        };
+        if (a == "--config") o.config = next();
+        else if (a == "--out") o.out = next();
+        else if (a == "--stdin") o.from_stdin = true;
+        else if (a == "--width") o.width = std::atoi(next().c_str());
+        else if (a == "--height") o.height = std::atoi(next().c_str());
+        else if (a == "--depth") o.depth = std::atoi(next().c_str());
+        else if (a == "--pitch") o.pitch = std::atof(next().c_str());
+        else if (a == "--device") o.device = std::atoi(next().c_str());
+        else { std::fprintf(stderr, "usage: rt_render [--config c1|c2|c3|c5 | --stdin] [--width W --height H "
+                                    "--pitch P --depth B] [--device N] [--out file.ppm]\n"); return 2; }
+    }
+
+    rt_scene scene;
+    std::vector<rt_sphere> spheres(RT_MAX_SPHERES);
+    std::vector<rt_light> lights(2);
+    int W, H, depth;
+    double pitch;
+    if (o.from_stdin) {
+        std::vector<std::string> sq;
+        std::vector<int32_t> ty;
+        read_dialogue(&sq, &ty);
+        std::vector<const char*> csq;
+        for (auto& s : sq) csq.push_back(s.c_str());
+        check(rt_load_scene(csq.data(), ty.data(), (int)csq.size(), &scene, spheres.data(), RT_MAX_SPHERES,
+                            &lights[0]),
+              "rt_load_scene");
+        W = o.width > 0 ? o.width : 500;                    // g_windowWidth/Height (:570)
+        H = o.height > 0 ? o.height : 500;
+        depth = o.depth >= 0 ? o.depth : 5;                 // MAX_DEPTH (:48)
+        pitch = o.pitch > 0 ? o.pitch : 1.0;                // rayTraceScreen's unit pixel step
+    } else {
+        Canonical c = canonical(o.config);
+        check(rt_scene_init_reference(&scene), "rt_scene_init_reference");
+        static const char* kSq[8] = {"d7", "b2", "f5", "h8", "c4", "e2", "g6", "a5"};
+        int n = 0;
+        if (c.nsph == 64) {
+            for (int r = 0; r < 8; ++r)
+                for (int cc = 0; cc < 8; ++cc) {
+                    char s[3] = {(char)('a' + r), (char)('1' + cc), 0};
+                    check(rt_convert_string_coordinate(s, spheres[n].center), "rt_convert_string_coordinate");
+                    spheres[n].center[0] += 0.0;
+                    spheres[n].center[1] += (double)(((r + cc) % 3) * 25);
+                    spheres[n].center[2] += 0.0;
+                    spheres[n].radius = 10.0;
+                    ++n;
+                }
+        } else {
+            for (; n < c.nsph; ++n) {
+                check(rt_convert_string_coordinate(kSq[n], spheres[n].center), "rt_convert_string_coordinate");
+                spheres[n].radius = 20.0;
+            }
+        }
+        const char* lsq[2] = {"b6", "g3"};
+        const double lcol[2] = {1.0, 0.5};
+        for (int k = 0; k < c.nl; ++k) {
+            check(rt_light_position_from_square(lsq[k], lights[k].position), "rt_light_position_from_square");
+            for (int q = 0; q < 3; ++q) lights[k].color[q] = lcol[k];
+        }
+        scene.n_spheres = n;
+        scene.spheres = spheres.data();
+        scene.n_lights = c.nl;
+        scene.lights = lights.data();
+        W = o.width > 0 ? o.width : c.w;
+        H = o.height > 0 ? o.height : c.h;
+        depth = o.depth >= 0 ? o.depth : c.depth;
+        pitch = o.pitch > 0 ? o.pitch : 500.0 / W;          // canonical framing
+    }
+
+    rt_camera cam;
+    check(rt_camera_init_reference(&cam, W, H, pitch), "rt_camera_init_reference");
+    rt_ctx* ctx = nullptr;
+    check(rt_ctx_create(o.device, &ctx), "rt_ctx_create");
+    std::vector<uint8_t> rgba8((size_t)W * H * 4);
+    rt_stats st;
+    check(rt_render(ctx, &scene, &cam, W, H, depth, nullptr, nullptr, rgba8.data(), nullptr, &st), "rt_render");
+    check(rt_write_ppm(o.out.c_str(), rgba8.data(), W, H, 4), "rt_write_ppm");
+    const uint64_t rays = st.primary_rays + st.reflect_rays + st.shadow_rays;
+    std::printf("rt_render: %dx%d depth %d -> %s | rays %llu (primary %llu, reflect %llu, shadow %llu) | kernel %.3f ms"
+                " | %.1f Mray/s\n",
+                W, H, depth, o.out.c_str(), (unsigned long long)rays, (unsigned long long)st.primary_rays,
+                (unsigned long long)st.reflect_rays, (unsigned long long)st.shadow_rays, st.kernel_ms,
+                rays / (st.kernel_ms * 1e3));
+    rt_ctx_destroy(ctx);
+    return 0;
+}

@@ -238,3 +238,45 @@ def test_host_buffer_render_and_stats(tr):
     assert st.primary_rays + st.reflect_rays + st.shadow_rays == scenes.PINNED_RAYS["c2"]
     assert st.primary_rays == cfg.width * cfg.height
     assert st.kernel_ms > 0
+
+
+def _ppm_expect(rgb64):
+    q = np.floor(np.clip(rgb64, 0.0, 1.0) * 255.0 + 0.5).astype(np.uint8)
+    return q[::-1]                       # writePpmScreenshot writes the bottom-up image top-down
+
+
+def _read_ppm(path):
+    data = open(path, "rb").read()
+    parts = data.split(b"\n", 1)
+    hdr = parts[0].split()
+    assert hdr[0] == b"P6" and hdr[3] == b"255"
+    W, H = int(hdr[1]), int(hdr[2])
+    return np.frombuffer(parts[1], np.uint8).reshape(H, W, 3)
+
+
+def test_cli_canonical_scene_ppm(tmp_path):
+    import subprocess
+    exe = os.path.join(os.path.dirname(abi.LIB_PATH), "rt_render")
+    out = tmp_path / "c1.ppm"
+    r = subprocess.run([exe, "--config", "c1", "--out", str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert f"rays {scenes.PINNED_RAYS['c1']}" in r.stdout
+    cfg = scenes.CONFIGS["c1"]
+    want, _ = po.render(cfg.scene().to_abi(), cfg.camera(), cfg.width, cfg.height, cfg.depth)
+    assert np.array_equal(_read_ppm(out), _ppm_expect(want))
+
+
+def test_cli_initscene2_dialogue_ppm(tmp_path):
+    """initScene2's stdin dialogue (MySdlApplication.cpp:1430-1493) -> loadScene -> draw() at the
+    reference's own window (500x500, unit pitch, MAX_DEPTH 5)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(abi.LIB_PATH), "rt_render")
+    answers = "d\nd7\ny\nzz\nd\nb2\nyes\na\nb6\nmaybe\nn\n"
+    out = tmp_path / "app.ppm"
+    r = subprocess.run([exe, "--stdin", "--out", str(out)], input=answers, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    sc = scenes.load_scene([("d7", scenes.SPHERE), ("b2", scenes.SPHERE), ("b6", scenes.LIGHT)])
+    cam = scenes.make_camera(500, 500, 1.0)
+    want, _ = po.render(sc.to_abi(), cam, 500, 500, 5)
+    assert np.array_equal(_read_ppm(out), _ppm_expect(want))
