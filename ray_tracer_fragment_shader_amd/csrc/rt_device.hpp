@@ -45,22 +45,32 @@ __device__ __forceinline__ double len(d3 a) { return sqrt(a.x * a.x + a.y * a.y 
 __device__ __forceinline__ d3 divs(d3 a, double l) { return mk(a.x / l, a.y / l, a.z / l); }      // :175
 __device__ __forceinline__ d3 ld3(const double* p) { return mk(p[0], p[1], p[2]); }
 
-// Where the kernels read the scene from (LDS copy or the global record).
+// Where the kernels read the scene from.  `S`, `sph`, `prim` (header and FP64 exact records) live in
+// LDS in the render kernel (or in global memory for the ray-list kernels); the FP32 filter images `sphf`,
+// `primf` are always read from global memory with wave-uniform indices, i.e. through the scalar cache
+// into SGPR operands.
 struct SceneView {
     const DevScene* S;
     const DevSphere* sph;
+    const DevSpherePrim* prim;
     const DevSphereF* sphf;
-    const DevSpherePrim* prim;      // primary-ray data (render kernel only; may be null)
     const DevSpherePrimF* primf;
+    int np;                          // padded sphere count (wave-uniform)
+    int nl;                          // light count (wave-uniform)
 };
 
-__device__ __forceinline__ SceneView view_of(const DevScene* S) {
+// hdr: header copy the kernel reads (LDS or global); g: the global record (for the filter images).
+__device__ __forceinline__ SceneView view_of(const DevScene* hdr, const DevScene* g, int np, int nl) {
     SceneView v;
-    v.S = S;
-    v.sph = reinterpret_cast<const DevSphere*>(S + 1);
-    v.sphf = reinterpret_cast<const DevSphereF*>(v.sph + S->n_spheres);
-    v.prim = nullptr;
-    v.primf = nullptr;
+    v.S = hdr;
+    v.np = np;
+    v.nl = nl;
+    v.sph = reinterpret_cast<const DevSphere*>(hdr + 1);
+    v.prim = reinterpret_cast<const DevSpherePrim*>(v.sph + np);
+    const DevSphere* gsph = reinterpret_cast<const DevSphere*>(g + 1);
+    const DevSpherePrim* gprim = reinterpret_cast<const DevSpherePrim*>(gsph + np);
+    v.sphf = reinterpret_cast<const DevSphereF*>(gprim + np);
+    v.primf = reinterpret_cast<const DevSpherePrimF*>(v.sphf + np);
     return v;
 }
 
@@ -181,6 +191,29 @@ __device__ __forceinline__ bool sphere_hit(const DevSphere& sp, d3 p0, d3 u, dou
 
 // Closest hit of g_scene (:796-821): Euclidean distance |p - p0|, strict <, board (child 0) first.
 // kind: -1 miss, 0 board, 1 + k sphere k.
+// Spheres go in batches of kChunk: the FP32 filter of the whole batch is evaluated branch-free (records
+// in SGPRs), then each lane runs the exact FP64 test only on its own surviving spheres, in increasing k,
+// so the strict-< closest-hit order of the reference is unchanged.  Padding spheres never survive.
+__device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const Ray& r, int k0, double eps,
+                                                     int* kind, double* best, d3* hp) {
+    uint32_t pass = 0;
+#pragma unroll
+    for (int j = 0; j < kChunk; ++j) pass |= (sphere_reject32(V.sphf[k0 + j], r) ? 0u : 1u) << j;
+    while (pass) {
+        const int k = k0 + __builtin_ctz(pass);
+        pass &= pass - 1;
+        d3 q;
+        if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) {
+            double dist = len(sub(q, r.p0));                // :811-812
+            if (dist < *best || *best < 0.0) {              // :813
+                *best = dist;
+                *kind = 1 + k;
+                *hp = q;
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3* hp) {
     const DevScene* S = V.S;
     if (!bound_pass(S, r.p0, r.u)) return -1;
@@ -194,24 +227,13 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
             *hp = q;
         }
     }
-    const int ns = S->n_spheres;
     const double eps = S->eps;
-    for (int k = 0; k < ns; ++k) {
-        if (sphere_reject32(V.sphf[k], r)) continue;
-        d3 q;
-        if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) {
-            double dist = len(sub(q, r.p0));                // :811-812
-            if (dist < best || best < 0.0) {                // :813
-                best = dist;
-                kind = 1 + k;
-                *hp = q;
-            }
-        }
-    }
+    for (int k0 = 0; k0 < V.np; k0 += kChunk) sphere_batch_closest(V, r, k0, eps, &kind, &best, hp);
     return kind;
 }
 
-// Closest hit of a primary ray Line(eye, sp): deltaP and |deltaP|^2 per sphere come from LDS.
+// Closest hit of a primary ray Line(eye, sp): deltaP and |deltaP|^2 per sphere were computed for this
+// eye by rt_prepare_kernel with the reference's operations (:740, :750).
 __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray& r, d3 bdP, double bdd,
                                                    d3* hp) {
     const DevScene* S = V.S;
@@ -226,22 +248,29 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
             *hp = q;
         }
     }
-    const int ns = S->n_spheres;
     const double eps = S->eps;
-    for (int k = 0; k < ns; ++k) {
-        const DevSpherePrimF& f = V.primf[k];
-        float uD = r.ux * f.dx;
-        uD = fmaf(r.uy, f.dy, uD);
-        uD = fmaf(r.uz, f.dz, uD);
-        if (fmaf(uD, uD, f.c0) < 0.0f) continue;           // certain disc < 0 (margin: rt_kernel.hip)
-        const DevSpherePrim& pp = V.prim[k];
-        d3 q;
-        if (sphere_hit_dp(ld3(pp.dP), pp.dd, V.sph[k].r2, r.p0, r.u, eps, &q)) {
-            double dist = len(sub(q, r.p0));
-            if (dist < best || best < 0.0) {
-                best = dist;
-                kind = 1 + k;
-                *hp = q;
+    for (int k0 = 0; k0 < V.np; k0 += kChunk) {
+        uint32_t pass = 0;
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            const DevSpherePrimF& f = V.primf[k0 + j];
+            float uD = r.ux * f.dx;
+            uD = fmaf(r.uy, f.dy, uD);
+            uD = fmaf(r.uz, f.dz, uD);
+            pass |= (fmaf(uD, uD, f.c0) < 0.0f ? 0u : 1u) << j;   // < 0: certain disc < 0
+        }
+        while (pass) {
+            const int k = k0 + __builtin_ctz(pass);
+            pass &= pass - 1;
+            const DevSpherePrim& pp = V.prim[k];
+            d3 q;
+            if (sphere_hit_dp(ld3(pp.dP), pp.dd, V.sph[k].r2, r.p0, r.u, eps, &q)) {
+                double dist = len(sub(q, r.p0));
+                if (dist < best || best < 0.0) {
+                    best = dist;
+                    kind = 1 + k;
+                    *hp = q;
+                }
             }
         }
     }
@@ -252,12 +281,17 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
 __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r) {
     const DevScene* S = V.S;
     if (!bound_pass(S, r.p0, r.u)) return false;
-    const int ns = S->n_spheres;
     const double eps = S->eps;
-    for (int k = 0; k < ns; ++k) {
-        if (sphere_reject32(V.sphf[k], r)) continue;
-        d3 q;
-        if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) return true;
+    for (int k0 = 0; k0 < V.np; k0 += kChunk) {
+        uint32_t pass = 0;
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) pass |= (sphere_reject32(V.sphf[k0 + j], r) ? 0u : 1u) << j;
+        while (pass) {
+            const int k = k0 + __builtin_ctz(pass);
+            pass &= pass - 1;
+            d3 q;
+            if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) return true;
+        }
     }
     if (S->has_board) {
         d3 q;
@@ -295,8 +329,7 @@ __device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 
     Ray sr;
     sr.p0 = p;
     set_origin_f32(S, &sr);
-    const int nl = S->n_lights;
-    for (int i = 0; i < nl; ++i) {
+    for (int i = 0; i < V.nl; ++i) {
         d3 lpos = ld3(S->light[i].pos);
         d3 sd = sub(lpos, p);                               // shadowRay end - start (:1216)
         double dl = len(sd);                                // shadowRay.length()
@@ -348,7 +381,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                 d3 rd = sub(pe, p);                         // reflectedRay = Line(p, p + r)
                 d3 rdir = divs(rd, len(rd));                // reflectedRay.direction()
                 local[lvl] = shade(V, p, n, mat, r.u, rdir);
-                nsh += S->n_lights;
+                nsh += V.nl;
                 levels = lvl + 1;
                 r.p0 = p;                                   // next level traces the reflected ray
                 set_dir(&r, rd, rdir);

@@ -227,10 +227,17 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
                            "rt_set_scene: transparent materials (transmitted rays) are outside the GPU path");
 
     const size_t bytes = (size_t)rt::scene_bytes_for(s->n_spheres);
+    const int np = rt::padded_spheres(s->n_spheres);
     blob->assign(bytes, 0);
     rt::DevScene* d = reinterpret_cast<rt::DevScene*>(blob->data());
     rt::DevSphere* sph = reinterpret_cast<rt::DevSphere*>(d + 1);
-    rt::DevSphereF* sphf = reinterpret_cast<rt::DevSphereF*>(sph + s->n_spheres);
+    rt::DevSpherePrim* prim = reinterpret_cast<rt::DevSpherePrim*>(sph + np);
+    rt::DevSphereF* sphf = reinterpret_cast<rt::DevSphereF*>(prim + np);
+    (void)prim;                                      // per-eye data: filled on the device (rt_prepare_kernel)
+    d->n_padded = np;
+    d->lds_bytes = rt::lds_bytes_for(s->n_spheres);
+    const double inf = std::numeric_limits<double>::infinity();
+    d->eye[0] = d->eye[1] = d->eye[2] = std::numeric_limits<double>::quiet_NaN();
 
     const HP zero = hp(0.0, 0.0, 0.0);
     const HP bc = hp(s->position) + zero;                                       // g_scene: _position + offset (:739)
@@ -320,6 +327,10 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
         float rmf = (float)rm;
         if ((double)rmf < rm) rmf = std::nextafter(rmf, std::numeric_limits<float>::infinity());
         sphf[k].rm = rmf;
+    }
+    for (int k = s->n_spheres; k < np; ++k) {                                   // padding: never a hit
+        sph[k].r2 = -inf;
+        sphf[k].rm = -std::numeric_limits<float>::infinity();
     }
     return RT_OK;
 }

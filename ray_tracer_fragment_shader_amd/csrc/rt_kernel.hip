@@ -46,8 +46,10 @@ struct RenderParams {
     int32_t width, height;
     int32_t local_rows;
     int32_t band_height, n_ranks, rank;
-    int32_t scene_bytes;
-    int32_t n_spheres;
+    int32_t lds_bytes;
+    int32_t np;
+    int32_t nl;
+    int32_t pad;
 };
 
 __device__ __forceinline__ int global_row_of(const RenderParams& P, int lr) {
@@ -76,50 +78,23 @@ __global__ __launch_bounds__(kThreads) void rt_render_kernel(const DevScene* __r
                                                              uint32_t* __restrict__ outrc) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
-    const int ns = P.n_spheres;
-    // LDS: [scene record (LDS = 1)] [DevSpherePrim[ns] | DevSpherePrimF[ns]] [output staging 12 KB]
+    // LDS: [header | DevSphere[np] | DevSpherePrim[np]] (LDS = 1) then the output staging tile (12 KB).
+    // The scene record is broadcast into LDS once per workgroup; the FP32 filter images stay in global
+    // memory and are read with wave-uniform indices (scalar loads, SGPR operands).
     int off = 0;
     const DevScene* S = gscene;
     if (LDS) {
-        stage_scene(smem, gscene, P.scene_bytes);
+        stage_scene(smem, gscene, P.lds_bytes);
         S = reinterpret_cast<const DevScene*>(smem);
-        off = P.scene_bytes;
+        off = P.lds_bytes;
     }
-    DevSpherePrim* prim = reinterpret_cast<DevSpherePrim*>(smem + off);
-    DevSpherePrimF* primf = reinterpret_cast<DevSpherePrimF*>(prim + ns);
-    off += prim_bytes_for(ns);
     float4* st32 = reinterpret_cast<float4*>(smem + off);                              // [8][32] 4 KB
     double* st64 = reinterpret_cast<double*>(smem + off + 4096);                        // [8][32][3] 6 KB
     uint32_t* strc = reinterpret_cast<uint32_t*>(smem + off + 4096 + 6144);             // [8][32] 1 KB
     uchar4* st8 = reinterpret_cast<uchar4*>(smem + off + 4096 + 6144 + 1024);           // [8][32] 1 KB
-
-    // Primary-ray sphere data for this frame's camera, once per workgroup: deltaP = C - eye and
-    // dot(deltaP, deltaP) exactly as Shape::intersection computes them for p0 = camera (:740, :750), and
-    // the FP32 filter image f32(deltaP), c0 = r2 - dd + K (S0^2 + r2) rounded up, S0 = max|deltaP_i|.
-    // Filter error < 35 eps32 S0^2 + 2 eps32 r2 << K (S0^2 + r2), K = 256 eps32.
+    if (LDS) __syncthreads();
+    const SceneView V = view_of(S, gscene, P.np, P.nl);
     const d3 eye = ld3(P.eye);
-    {
-        const DevSphere* gsph = reinterpret_cast<const DevSphere*>(gscene + 1);
-        for (int k = tid; k < ns; k += kThreads) {
-            d3 dP = sub(ld3(gsph[k].c), eye);
-            double dd = dot(dP, dP);
-            DevSpherePrim pp;
-            pp.dP[0] = dP.x; pp.dP[1] = dP.y; pp.dP[2] = dP.z;
-            pp.dd = dd;
-            prim[k] = pp;
-            double s0 = fmax(fabs(dP.x), fmax(fabs(dP.y), fabs(dP.z)));
-            double r2 = gsph[k].r2;
-            double c0 = (r2 - dd) + (double)kFilterK * (s0 * s0 + r2);
-            DevSpherePrimF f;
-            f.dx = (float)dP.x; f.dy = (float)dP.y; f.dz = (float)dP.z;
-            f.c0 = __double2float_ru(c0);
-            primf[k] = f;
-        }
-    }
-    __syncthreads();
-    SceneView V = view_of(S);
-    V.prim = prim;
-    V.primf = primf;
 
     const int wave = tid >> 6, lane = tid & 63;
     const int cx = wave * 8 + (lane & 7);          // column inside the 32 x 8 tile
@@ -164,6 +139,37 @@ __global__ __launch_bounds__(kThreads) void rt_render_kernel(const DevScene* __r
     }
 }
 
+// Per-eye primary-ray sphere data (run by rt_render_dev when the camera eye changes): deltaP = C - eye
+// and dot(deltaP, deltaP) exactly as Shape::intersection computes them for p0 = camera (:740, :750), and
+// the FP32 filter image f32(deltaP), c0 = (r2 - dd) + K (S0^2 + r2) rounded up, S0 = max|deltaP_i|.
+// Filter error < 35 eps32 S0^2 + 2 eps32 r2 << K (S0^2 + r2), K = 256 eps32.  Padding spheres have
+// r2 = -inf, hence c0 = -inf: always rejected.
+__global__ __launch_bounds__(kThreads) void rt_prepare_kernel(DevScene* __restrict__ g, double ex, double ey,
+                                                              double ez) {
+    const int np = g->n_padded;
+    DevSphere* sph = reinterpret_cast<DevSphere*>(g + 1);
+    DevSpherePrim* prim = reinterpret_cast<DevSpherePrim*>(sph + np);
+    DevSphereF* sphf = reinterpret_cast<DevSphereF*>(prim + np);
+    DevSpherePrimF* primf = reinterpret_cast<DevSpherePrimF*>(sphf + np);
+    const d3 eye = mk(ex, ey, ez);
+    const int k = blockIdx.x * kThreads + threadIdx.x;
+    if (k == 0) { g->eye[0] = ex; g->eye[1] = ey; g->eye[2] = ez; }
+    if (k >= np) return;
+    d3 dP = sub(ld3(sph[k].c), eye);
+    double dd = dot(dP, dP);
+    DevSpherePrim pp;
+    pp.dP[0] = dP.x; pp.dP[1] = dP.y; pp.dP[2] = dP.z;
+    pp.dd = dd;
+    prim[k] = pp;
+    double s0 = fmax(fabs(dP.x), fmax(fabs(dP.y), fabs(dP.z)));
+    double r2 = sph[k].r2;
+    double c0 = (r2 - dd) + (double)kFilterK * (s0 * s0 + r2);
+    DevSpherePrimF f;
+    f.dx = (float)dP.x; f.dy = (float)dP.y; f.dz = (float)dP.z;
+    f.c0 = __double2float_ru(c0);
+    primf[k] = f;
+}
+
 template <int B>
 __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene* __restrict__ S,
                                                                  const double* __restrict__ starts,
@@ -173,7 +179,8 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
     const int k = blockIdx.x * kThreads + threadIdx.x;
     if (k >= n) return;
     uint32_t seg = 0, sh = 0;
-    d3 c = trace<B, false>(view_of(S), ld3(starts + 3 * k), ld3(ends + 3 * k), mk(0.0, 0.0, 0.0), 0.0, &seg, &sh);
+    const SceneView V = view_of(S, S, S->n_padded, S->n_lights);
+    d3 c = trace<B, false>(V, ld3(starts + 3 * k), ld3(ends + 3 * k), mk(0.0, 0.0, 0.0), 0.0, &seg, &sh);
     if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
     if (rc) rc[k] = seg | (sh << 16);
 }
@@ -184,7 +191,7 @@ __global__ __launch_bounds__(kThreads) void rt_intersect_kernel(const DevScene* 
                                                                 rt_hit* __restrict__ hits) {
     const int k = blockIdx.x * kThreads + threadIdx.x;
     if (k >= n) return;
-    const SceneView V = view_of(S);
+    const SceneView V = view_of(S, S, S->n_padded, S->n_lights);
     Ray r;
     r.p0 = ld3(starts + 3 * k);
     d3 d = sub(ld3(ends + 3 * k), r.p0);
@@ -270,9 +277,13 @@ struct rt_ctx {
     DevScene* d_scene = nullptr;
     size_t scene_cap = 0;
     int scene_bytes = 0;
-    int n_spheres = 0;
+    int lds_bytes = 0;
+    int n_padded = 0;
+    int n_lights = 0;
     bool scene_set = false;
-    int use_lds = 1;
+    bool eye_valid = false;                    // the device *Prim arrays hold data for `eye`
+    double eye[3] = {0, 0, 0};
+    int use_lds = 0;                           // RT_SCENE_IN_LDS=1: header + exact records in LDS (A/B: tools/ab.py)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -339,7 +350,11 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     }
     RT_HIP(hipMemcpy(c->d_scene, blob.data(), blob.size(), hipMemcpyHostToDevice));
     c->scene_bytes = (int)blob.size();
-    c->n_spheres = reinterpret_cast<const rt::DevScene*>(blob.data())->n_spheres;
+    const rt::DevScene* h = reinterpret_cast<const rt::DevScene*>(blob.data());
+    c->lds_bytes = h->lds_bytes;
+    c->n_padded = h->n_padded;
+    c->n_lights = h->n_lights;
+    c->eye_valid = false;
     c->scene_set = true;
     return RT_OK;
 }
@@ -373,8 +388,9 @@ static int render_params(const rt_ctx* c, const rt_camera* cam, int W, int H, in
     P->band_height = banded ? rows->band_height : H;
     P->n_ranks = banded ? rows->n_ranks : 1;
     P->rank = banded ? rows->rank : 0;
-    P->scene_bytes = c->scene_bytes;
-    P->n_spheres = c->n_spheres;
+    P->lds_bytes = c->lds_bytes;
+    P->np = c->n_padded;
+    P->nl = c->n_lights;
     return RT_OK;
 }
 
@@ -388,11 +404,23 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     const int tiles_x = (W + kTileW - 1) / kTileW;
     const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
     dim3 grid((unsigned)(tiles_x * tiles_y));
-    const size_t stage = (size_t)prim_bytes_for(c->n_spheres) + 4096 + 6144 + 1024 + 1024;
+    const size_t stage = 4096 + 6144 + 1024 + 1024;
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
+    // Primary-ray sphere data for this eye (stream-ordered; only when the eye changes).
+    if (!c->eye_valid || memcmp(c->eye, cam->eye, sizeof(c->eye)) != 0) {
+        if (c->n_padded > 0) {
+            dim3 pg((unsigned)((c->n_padded + kThreads - 1) / kThreads));
+            hipLaunchKernelGGL(rt_prepare_kernel, pg, dim3(kThreads), 0, st, c->d_scene, cam->eye[0], cam->eye[1],
+                               cam->eye[2]);
+            e = hipGetLastError();
+            if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_prepare_kernel: ") + hipGetErrorString(e));
+        }
+        memcpy(c->eye, cam->eye, sizeof(c->eye));
+        c->eye_valid = true;
+    }
     if (c->use_lds)
-        e = launch_render_lds<1>(depth, grid, c->scene_bytes + stage, st, c->d_scene, P,
+        e = launch_render_lds<1>(depth, grid, c->lds_bytes + stage, st, c->d_scene, P,
                                  reinterpret_cast<float4*>(rgba32f), reinterpret_cast<uchar4*>(rgba8), rgb64f,
                                  raycount);
     else

@@ -1,14 +1,21 @@
 // rt_layout.hpp — the device scene record (plain C++, shared by the host builder and the kernels).
 //
-// Layout in HBM (one allocation per rt_ctx, uploaded by rt_set_scene):
-//   DevScene header | DevSphere[n] (FP64 exact data) | DevSphereF[n] (FP32 filter data)
-// Per workgroup the kernel copies the record into LDS and appends, computed in its prologue for the
-// frame's camera, DevSpherePrim[n] | DevSpherePrimF[n] (primary-ray data, see rt_device.hpp).
+// Layout in HBM (one allocation per rt_ctx):
+//   DevScene header
+//   DevSphere[np]       FP64 exact data                 ┐ copied into LDS once per workgroup
+//   DevSpherePrim[np]   primary-ray FP64 data (per eye)  ┘ (lds_bytes)
+//   DevSphereF[np]      FP32 filter image               ┐ read through the scalar cache (SGPR operands),
+//   DevSpherePrimF[np]  primary-ray FP32 filter (per eye)┘ 8 records per s_load batch
+// np = n_spheres rounded up to kChunk; the padding spheres have r2 = -inf and filter terms = -inf, so
+// they are rejected by the filter and can never hit.  The two *Prim arrays depend on the camera eye and
+// are (re)written on the device by rt_prepare_kernel whenever rt_render_dev sees a new eye.
 #pragma once
 
 #include <stdint.h>
 
 namespace rt {
+
+constexpr int kChunk = 4;              // spheres per branch-free filter batch
 
 // FP32 filter margin factor: 256 unit roundoffs of binary32.  The filter's own error is below
 // 64 * 2^-24 * (S^2 + r^2) (error budget in rt_device.hpp, sphere_reject32), so a margin of
@@ -38,13 +45,13 @@ struct alignas(16) DevSphere {         // world centre = _position + positionOff
     double r2;
 };
 
-struct alignas(16) DevSphereF {        // FP32 filter: centre - bound centre, r2 + 4K*sC^2 + K*r2 (rounded up)
-    float cx, cy, cz, rm;
-};
-
 struct alignas(16) DevSpherePrim {     // primary rays: deltaP = C - eye and dot(deltaP, deltaP) (:740, :750)
     double dP[3];
     double dd;
+};
+
+struct alignas(16) DevSphereF {        // FP32 filter: centre - bound centre, r2 + 4K*sC^2 + K*r2 (rounded up)
+    float cx, cy, cz, rm;
 };
 
 struct alignas(16) DevSpherePrimF {    // FP32 filter for primary rays: f32(dP), r2 - dd + K*(S0^2 + r2)
@@ -60,22 +67,27 @@ struct alignas(16) DevScene {
     double coff[3];                    // checker offset = positionOffset of CheckerBoard (:1101)
     double half;                       // BOARD_HALF_SIZE
     double square;                     // SQUARE_EDGE_SIZE
+    double eye[3];                     // camera the *Prim arrays were computed for
     int32_t bound_on;                  // g_scene radius > 0
     int32_t has_board;
-    int32_t n_spheres;
+    int32_t n_spheres;                 // real spheres
+    int32_t n_padded;                  // np: n_spheres rounded up to kChunk
     int32_t n_lights;
+    int32_t lds_bytes;                 // header + DevSphere[np] + DevSpherePrim[np]
+    int32_t pad0, pad1;
     DevTri tri[2];                     // board triangles T1 = (P1,P2,P3), T2 = (P1,P3,P4)   (:840-841)
     DevMat mat[3];                     // 0 white square, 1 black square, 2 sphere
     DevLight light[16];
-    // followed by n_spheres DevSphere, then n_spheres DevSphereF
 };
 
-inline constexpr int scene_bytes_for(int n_spheres) {
-    return (int)(sizeof(DevScene) + (sizeof(DevSphere) + sizeof(DevSphereF)) * (unsigned)n_spheres);
+inline constexpr int padded_spheres(int n) { return (n + kChunk - 1) / kChunk * kChunk; }
+
+inline constexpr int lds_bytes_for(int n) {
+    return (int)(sizeof(DevScene) + (sizeof(DevSphere) + sizeof(DevSpherePrim)) * (unsigned)padded_spheres(n));
 }
 
-inline constexpr int prim_bytes_for(int n_spheres) {
-    return (int)((sizeof(DevSpherePrim) + sizeof(DevSpherePrimF)) * (unsigned)n_spheres);
+inline constexpr int scene_bytes_for(int n) {
+    return lds_bytes_for(n) + (int)((sizeof(DevSphereF) + sizeof(DevSpherePrimF)) * (unsigned)padded_spheres(n));
 }
 
 }  // namespace rt
