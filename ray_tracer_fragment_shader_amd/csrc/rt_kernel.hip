@@ -70,8 +70,8 @@ __device__ __forceinline__ unsigned char to_u8(double c) {
     return (unsigned char)(int)floor(v * 255.0 + 0.5);
 }
 
-template <int B, int LDS>
-__global__ __launch_bounds__(kThreads) void rt_render_kernel(const DevScene* __restrict__ gscene,
+template <int B, int LDS, int MINW>
+__global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
                                                              RenderParams P, float4* __restrict__ out32,
                                                              uchar4* __restrict__ out8,
                                                              double* __restrict__ out64,
@@ -232,17 +232,17 @@ __global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* 
 
 // ------------------------------------------------------------------------------------------------
 // Template dispatch.
-template <int LDS>
+template <int LDS, int MINW>
 hipError_t launch_render_lds(int depth, dim3 grid, size_t lds, hipStream_t st, const DevScene* s,
                              const RenderParams& P, float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
 #define RT_CASE(b)                                                                                      \
     case b:                                                                                             \
         if (lds > 65536) {                                                                              \
-            hipError_t e_ = hipFuncSetAttribute((const void*)rt_render_kernel<b, LDS>,                  \
+            hipError_t e_ = hipFuncSetAttribute((const void*)rt_render_kernel<b, LDS, MINW>,                  \
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);  \
             if (e_ != hipSuccess) return e_;                                                            \
         }                                                                                               \
-        hipLaunchKernelGGL((rt_render_kernel<b, LDS>), grid, dim3(kThreads), lds, st, s, P, o32, o8,    \
+        hipLaunchKernelGGL((rt_render_kernel<b, LDS, MINW>), grid, dim3(kThreads), lds, st, s, P, o32, o8,    \
                            o64, orc);                                                                   \
         break;
     switch (depth) {
@@ -283,6 +283,8 @@ struct rt_ctx {
     bool scene_set = false;
     bool eye_valid = false;                    // the device *Prim arrays hold data for `eye`
     double eye[3] = {0, 0, 0};
+    int min_waves = 5;                         // __launch_bounds__(256, 5) for depth <= 3 (measured faster
+                                               // despite small spills: tools/ab.py); RT_MIN_WAVES=0 disables
     int use_lds = 0;                           // RT_SCENE_IN_LDS=1: header + exact records in LDS (A/B: tools/ab.py)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
@@ -316,6 +318,7 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     rt_ctx* c = new rt_ctx();
     c->device = device;
     if (const char* e = getenv("RT_SCENE_IN_LDS")) c->use_lds = atoi(e) != 0;
+    if (const char* e = getenv("RT_MIN_WAVES")) c->min_waves = atoi(e);
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         delete c;
         return rt_fail(RT_EHIP, "rt_ctx_create: hipEventCreate failed");
@@ -420,11 +423,12 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
         c->eye_valid = true;
     }
     if (c->use_lds)
-        e = launch_render_lds<1>(depth, grid, c->lds_bytes + stage, st, c->d_scene, P,
+        e = launch_render_lds<1, 1>(depth, grid, c->lds_bytes + stage, st, c->d_scene, P,
                                  reinterpret_cast<float4*>(rgba32f), reinterpret_cast<uchar4*>(rgba8), rgb64f,
                                  raycount);
     else
-        e = launch_render_lds<0>(depth, grid, stage, st, c->d_scene, P, reinterpret_cast<float4*>(rgba32f),
+        e = (c->min_waves >= 5 && depth <= 3 ? launch_render_lds<0, 5> : launch_render_lds<0, 1>)(
+                depth, grid, stage, st, c->d_scene, P, reinterpret_cast<float4*>(rgba32f),
                                  reinterpret_cast<uchar4*>(rgba8), rgb64f, raycount);
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_kernel launch: ") + hipGetErrorString(e));
     return RT_OK;

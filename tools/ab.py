@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
-"""Interleaved in-process timing of rt_render_dev across configs and scene-placement modes
-(RT_SCENE_IN_LDS = 1 / 0).  Prints one JSON line per (config, mode) with median / min kernel ms."""
+"""Interleaved in-process timing of rt_render_dev across configs and kernel variants.
+
+usage: ab.py c1,c2,c3,c5 MODE[,MODE...]   where MODE is a '+'-joined list of env settings applied when the
+context is created, e.g. RT_SCENE_IN_LDS=1 or RT_MIN_WAVES=5+RT_SCENE_IN_LDS=0 ("base" = defaults).
+Prints one JSON line per (config, mode) with median / min kernel ms."""
 import json
 import os
 import statistics
@@ -17,13 +20,19 @@ from ray_tracer_fragment_shader_amd.tracer import Tracer  # noqa: E402
 
 def main():
     cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c1", "c2", "c3", "c5"]
-    modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "0"]
+    modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["base", "RT_SCENE_IN_LDS=1"]
     rounds = int(os.environ.get("ROUNDS", "5"))
     reps = int(os.environ.get("REPS", "10"))
     tracers = {}
     for m in modes:
-        os.environ["RT_SCENE_IN_LDS"] = m
+        saved = dict(os.environ)
+        if m != "base":
+            for kv in m.split("+"):
+                k, v = kv.split("=")
+                os.environ[k] = v
         tracers[m] = Tracer(0)
+        os.environ.clear()
+        os.environ.update(saved)
     res = {(c, m): [] for c in cfgs for m in modes}
     bufs = {}
     for c in cfgs:
@@ -48,7 +57,7 @@ def main():
     for (c, m), v in res.items():
         rays = scenes.PINNED_RAYS[c]
         med = statistics.median(v)
-        print(json.dumps({"config": c, "lds": m, "median_ms": round(med, 4), "min_ms": round(min(v), 4),
+        print(json.dumps({"config": c, "mode": m, "median_ms": round(med, 4), "min_ms": round(min(v), 4),
                           "Mray/s": round(rays / med / 1e3, 1)}))
 
 

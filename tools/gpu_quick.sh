@@ -7,4 +7,4 @@ timeout -k 10 900 python -m pytest tests -m gpu -q -x ${PYTEST_ARGS:-} > gpurun_
 rc=$?
 tail -15 gpurun_out/gpu_tests.log
 if [ $rc -ne 0 ]; then echo "pytest rc=$rc"; exit $rc; fi
-timeout -k 10 300 python tools/ab.py ${AB_CFGS:-c1,c2,c3,c5} ${AB_MODES:-1,0} 2>&1 | tee gpurun_out/ab.log
+timeout -k 10 300 python tools/ab.py ${AB_CFGS:-c1,c2,c3,c5} ${AB_MODES:-base,RT_SCENE_IN_LDS=1} 2>&1 | tee gpurun_out/ab.log
