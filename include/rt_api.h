@@ -31,17 +31,21 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 #define RT_OK            0
 #define RT_EINVAL       -1   /* bad argument (null pointer, size, unsupported material, ...) */
 #define RT_EHIP         -2   /* HIP runtime error or no device */
 #define RT_ENOMEM       -3   /* allocation failed */
-#define RT_EUNSUPPORTED -4   /* reference feature outside the GPU path (transparent materials, meshes) */
+#define RT_EUNSUPPORTED -4   /* reference feature outside the GPU path (cylinder/cone stubs, branching rays) */
 
 #define RT_MAX_SPHERES 1024
 #define RT_MAX_LIGHTS  16
+#define RT_MAX_MESHES  64
 #define RT_MAX_DEPTH   7     /* reference uses MAX_DEPTH = 5 (MySdlApplication.cpp:48) */
+
+#define RT_MESH_TETRAHEDRON 1   /* Tetrahedron(p, edgeSize), MySdlApplication.cpp:863-900 */
+#define RT_MESH_CUBE        2   /* Cube(p, edgeSize),        MySdlApplication.cpp:903-950 */
 
 /* Material — MySdlApplication.cpp:272-307 (ambient, diffuse, specular, transparency, refraction). */
 typedef struct rt_material {
@@ -65,9 +69,21 @@ typedef struct rt_light {
     double position[3];
 } rt_light;
 
+/* A triangle-mesh composite of the reference: a Shape with a bounding sphere of radius
+ * sqrt(3)*edge/2 around `position` and triangle sub-objects (tetrahedron: 4 triangles; cube: 6 Quads of
+ * 2 triangles), material g_tetrahedronMaterial / g_cubeMaterial.  `position` is scene-local, the `p`
+ * handed to the constructor.  g_scene child order: the mesh comes after `after_spheres` spheres (and
+ * after every mesh listed before it). */
+typedef struct rt_mesh {
+    int32_t kind;                /* RT_MESH_TETRAHEDRON or RT_MESH_CUBE */
+    int32_t after_spheres;
+    double position[3];
+    double edge;
+} rt_mesh;
+
 /* The reference's g_scene (MySdlApplication.cpp:590) flattened: a bounding sphere at `position` of
  * `radius`, then children in insertion order — the CheckerBoard first when present (initScene2 inserts
- * it first, MySdlApplication.cpp:1442-1443), then the spheres in the order given. */
+ * it first, MySdlApplication.cpp:1442-1443), then spheres and meshes in the order given (see rt_mesh). */
 typedef struct rt_scene {
     double position[3];          /* g_scene position, BOARD_POSITION (MySdlApplication.cpp:42) */
     double radius;               /* g_scene radius sqrt(3)*BOARD_HALF_SIZE; <= 0 disables the cull */
@@ -85,6 +101,11 @@ typedef struct rt_scene {
     rt_material sphere_material; /* g_sphereMaterial (MySdlApplication.cpp:586) */
     const rt_sphere* spheres;    /* host pointer, n_spheres entries */
     const rt_light* lights;      /* host pointer, n_lights entries (the per-frame `lights` vector) */
+    rt_material tetrahedron_material;  /* g_tetrahedronMaterial (MySdlApplication.cpp:587) */
+    rt_material cube_material;         /* g_cubeMaterial (MySdlApplication.cpp:588) */
+    int32_t n_meshes;            /* <= RT_MAX_MESHES */
+    int32_t reserved1;
+    const rt_mesh* meshes;       /* host pointer, n_meshes entries */
 } rt_scene;
 
 /* Camera — rayTraceScreen's arguments (MySdlApplication.cpp:1251-1252, called at :1560).
@@ -125,8 +146,9 @@ typedef struct rt_hit {
     double point[3];
     double normal[3];
     double reflected_end[3];     /* reflectedRay().endPoint() = point + r */
+    double transmitted_end[3];   /* transmittedRay().endPoint() = point + t (t = 0 on total reflection) */
     int32_t hit;                 /* Intersection::intersects() */
-    int32_t material;            /* 0 white square, 1 black square, 2 sphere, -1 none */
+    int32_t material;            /* 0 white square, 1 black square, 2 sphere, 3 tetrahedron, 4 cube, -1 none */
 } rt_hit;
 
 typedef struct rt_ctx rt_ctx;
@@ -150,11 +172,12 @@ int rt_light_position_from_square(const char* square, double out[3]);
 /* loadScene (MySdlApplication.cpp:1495-1539) over boardMap entries (square -> type; types as the
  * reference enum {LIGHT, TETRAHEDRON, CUBE, SPHERE, CYLINDER, CONE}, MySdlApplication.cpp:16).
  * Duplicate squares keep the last type (boardMap[tmp] = type, :1467), entries are visited in
- * std::map<string> order, the last light wins.  Spheres are written to sphere_buf (capacity
- * sphere_cap); the light (white, g_lightColor) to *light.  Returns RT_EUNSUPPORTED if a mesh type
- * (tetrahedron, cube, cylinder, cone) is present; spheres and light are still filled. */
+ * std::map<string> order, the last light wins.  Spheres go to sphere_buf (capacity sphere_cap),
+ * tetrahedra and cubes to mesh_buf (capacity mesh_cap) in child order, the light (white,
+ * g_lightColor) to *light.  Returns RT_EUNSUPPORTED if a cylinder or cone is present (their reference
+ * implementations are stubs: MySdlApplication.cpp:1000-1020, 457-458); everything else is still filled. */
 int rt_load_scene(const char* const* squares, const int32_t* types, int n, rt_scene* scene,
-                  rt_sphere* sphere_buf, int sphere_cap, rt_light* light);
+                  rt_sphere* sphere_buf, int sphere_cap, rt_mesh* mesh_buf, int mesh_cap, rt_light* light);
 /* draw()'s camera (MySdlApplication.cpp:1556-1560) for a W x H window at the given pitch. */
 int rt_camera_init_reference(rt_camera* cam, int width, int height, double pitch);
 /* Number of image rows a rank renders under `rows` (NULL = all rows). */

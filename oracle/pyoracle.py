@@ -72,7 +72,7 @@ def ref() -> ctypes.CDLL:
                 raise RuntimeError("reference build unavailable (no /root/reference here)")
             build(ref=True)
         L = ctypes.CDLL(REF_SO)
-        scene_args = [c_char_p, c_void_p, c_void_p, c_int, c_char_p, c_void_p, c_int]
+        scene_args = [c_char_p, c_int, c_void_p, c_void_p, c_void_p, c_char_p, c_void_p, c_int]
         L.ref_render.restype = c_int
         L.ref_render.argtypes = scene_args + [c_int, c_int, c_int, c_double, c_int, c_int, c_void_p, c_int]
         L.ref_render_pixels.restype = c_int
@@ -81,8 +81,8 @@ def ref() -> ctypes.CDLL:
         L.ref_trace_rays.restype = c_int
         L.ref_trace_rays.argtypes = scene_args + [c_void_p, c_void_p, c_int, c_int, c_void_p]
         L.ref_intersect.restype = c_int
-        L.ref_intersect.argtypes = [c_char_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                                    c_void_p, c_void_p]
+        L.ref_intersect.argtypes = [c_char_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                    c_void_p, c_void_p, c_void_p]
         L.ref_convert_string_coordinate.restype = None
         L.ref_convert_string_coordinate.argtypes = [c_char_p, c_void_p]
         _ref = L
@@ -139,10 +139,10 @@ def intersect(scene_abi, starts, ends):
 
 def hits_to_dict(hits, n):
     raw = np.frombuffer(hits, dtype=np.uint8, count=n * ctypes.sizeof(abi.rt_hit)).reshape(n, -1)
-    d = raw[:, :72].copy().view(np.float64).reshape(n, 9)
-    i = raw[:, 72:80].copy().view(np.int32).reshape(n, 2)
-    return {"point": d[:, 0:3], "normal": d[:, 3:6], "reflected_end": d[:, 6:9], "hit": i[:, 0],
-            "material": i[:, 1]}
+    d = raw[:, :96].copy().view(np.float64).reshape(n, 12)
+    i = raw[:, 96:104].copy().view(np.int32).reshape(n, 2)
+    return {"point": d[:, 0:3], "normal": d[:, 3:6], "reflected_end": d[:, 6:9], "transmitted_end": d[:, 9:12],
+            "hit": i[:, 0], "material": i[:, 1]}
 
 
 def camera_basis(cam):
@@ -197,10 +197,11 @@ def ref_intersect(scene, starts, ends):
     starts = np.ascontiguousarray(starts, np.float64)
     ends = np.ascontiguousarray(ends, np.float64)
     n = starts.shape[0]
-    out9 = np.zeros((n, 9), np.float64)
+    out12 = np.zeros((n, 12), np.float64)
     hit = np.zeros(n, np.int32)
     mat = np.zeros(n, np.int32)
     a = scene.ref_args()
-    ref().ref_intersect(a[0], a[1], a[2], a[3], _ptr(starts), _ptr(ends), n, _ptr(out9), _ptr(hit), _ptr(mat))
-    return {"point": out9[:, 0:3], "normal": out9[:, 3:6], "reflected_end": out9[:, 6:9], "hit": hit,
-            "material": mat}
+    ref().ref_intersect(a[0], a[1], a[2], a[3], a[4], _ptr(starts), _ptr(ends), n, _ptr(out12), _ptr(hit),
+                        _ptr(mat))
+    return {"point": out12[:, 0:3], "normal": out12[:, 3:6], "reflected_end": out12[:, 6:9],
+            "transmitted_end": out12[:, 9:12], "hit": hit, "material": mat}

@@ -2,8 +2,10 @@
 // hot-path source ranges by oracle/Makefile, so every class and function used below is the reference's).
 //
 // Scenes are built exactly the way the reference app builds them (loadScene, MySdlApplication.cpp:
-// 1495-1539): a g_scene-like Shape (:590), CheckerBoard(Point(0,0,0)) first (:1442-1443), then
-// Sphere(convertStringCoordinate(sq) [+ (0,yoff,0)], r) in order, Light(color, BOARD_POSITION +
+// 1495-1539): a g_scene-like Shape (:590), CheckerBoard(Point(0,0,0)) first (:1442-1443), then the
+// children in the order of `children` (3-char tokens: 'S'|'T'|'C' + square): Sphere(
+// convertStringCoordinate(sq) [+ (0,yoff,0)], r), Tetrahedron(convertStringCoordinate(sq), edge),
+// Cube(convertStringCoordinate(sq), edge); lights Light(color, BOARD_POSITION +
 // (0,3.5*SQUARE_EDGE_SIZE,0) + convertStringCoordinate(sq)) (:1511).  Pixels use the deterministic
 // primary ray of SURVEY.md Appendix B with the rayTraceScreen basis (:1270-1279) and are shaded by the
 // reference rayTraceRay (:1184-1249).
@@ -17,16 +19,25 @@ struct RefScene {
     vector<Light> lights;
 };
 
-RefScene build(const char* sph_sq, const double* sph_yoff, const double* sph_r, int n_sph,
-               const char* light_sq, const double* light_col, int n_lights) {
+RefScene build(const char* children, int n_children, const double* sph_yoff, const double* sph_r,
+               const double* mesh_edge, const char* light_sq, const double* light_col, int n_lights) {
     RefScene r;
     r.scene = new Shape(Point(BOARD_POSITION), Material(), sqrt((double)3) * BOARD_HALF_SIZE, false);
     r.scene->addRayObject(new CheckerBoard(Point(0.0, 0.0, 0.0)));
-    for (int k = 0; k < n_sph; ++k) {
-        string sq(sph_sq + 2 * k, 2);
-        Point c = convertStringCoordinate(sq);
-        if (sph_yoff) c = c + Point(0.0, sph_yoff[k], 0.0);
-        r.scene->addRayObject(new Sphere(c, sph_r[k]));
+    int ks = 0, km = 0;
+    for (int c = 0; c < n_children; ++c) {
+        char type = children[3 * c];
+        string sq(children + 3 * c + 1, 2);
+        Point p = convertStringCoordinate(sq);
+        if (type == 'S') {
+            if (sph_yoff) p = p + Point(0.0, sph_yoff[ks], 0.0);
+            r.scene->addRayObject(new Sphere(p, sph_r[ks]));
+            ++ks;
+        } else if (type == 'T') {
+            r.scene->addRayObject(new Tetrahedron(p, mesh_edge[km++]));
+        } else {
+            r.scene->addRayObject(new Cube(p, mesh_edge[km++]));
+        }
     }
     for (int k = 0; k < n_lights; ++k) {
         string sq(light_sq + 2 * k, 2);
@@ -37,6 +48,8 @@ RefScene build(const char* sph_sq, const double* sph_yoff, const double* sph_r, 
 }
 
 int material_id(Material m) {
+    if (m.transparency().x() != 0) return 3;      // g_tetrahedronMaterial
+    if (m.ambient().y() == 0 && m.ambient().x() != 0) return 4;   // g_cubeMaterial (red)
     if (m.specular().x() == 0) return 1;          // g_blackSquare
     if (m.ambient().x() != 0) return 0;           // g_whiteSquare
     return 2;                                     // g_sphereMaterial
@@ -47,10 +60,11 @@ int material_id(Material m) {
 extern "C" {
 
 // Render rows [row_begin, row_end) of a W x H frame; rgb has (row_end-row_begin)*W*3 doubles.
-int ref_render(const char* sph_sq, const double* sph_yoff, const double* sph_r, int n_sph,
-               const char* light_sq, const double* light_col, int n_lights, int W, int H, int depth,
+int ref_render(const char* children, int n_children, const double* sph_yoff, const double* sph_r,
+               const double* mesh_edge, const char* light_sq, const double* light_col, int n_lights, int W, int H,
+               int depth,
                double pitch, int row_begin, int row_end, double* rgb, int nthreads) {
-    RefScene rs = build(sph_sq, sph_yoff, sph_r, n_sph, light_sq, light_col, n_lights);
+    RefScene rs = build(children, n_children, sph_yoff, sph_r, mesh_edge, light_sq, light_col, n_lights);
     Point camera(CAMERA_POSITION);
     Point lookAt(LOOK_AT_VECTOR);
     Point up(UP_VECTOR);
@@ -75,11 +89,11 @@ int ref_render(const char* sph_sq, const double* sph_yoff, const double* sph_r, 
 }
 
 // Sampled pixels (i[k], j[k]) of a W x H frame.
-int ref_render_pixels(const char* sph_sq, const double* sph_yoff, const double* sph_r, int n_sph,
-                      const char* light_sq, const double* light_col, int n_lights, int W, int H,
-                      int depth, double pitch, const int32_t* pi, const int32_t* pj, int n,
+int ref_render_pixels(const char* children, int n_children, const double* sph_yoff, const double* sph_r,
+                      const double* mesh_edge, const char* light_sq, const double* light_col, int n_lights,
+                      int W, int H, int depth, double pitch, const int32_t* pi, const int32_t* pj, int n,
                       double* rgb, int nthreads) {
-    RefScene rs = build(sph_sq, sph_yoff, sph_r, n_sph, light_sq, light_col, n_lights);
+    RefScene rs = build(children, n_children, sph_yoff, sph_r, mesh_edge, light_sq, light_col, n_lights);
     Point camera(CAMERA_POSITION);
     Point lookAt(LOOK_AT_VECTOR);
     Point up(UP_VECTOR);
@@ -102,10 +116,11 @@ int ref_render_pixels(const char* sph_sq, const double* sph_yoff, const double* 
 }
 
 // rayTraceRay on arbitrary rays Line(starts[k], ends[k]).
-int ref_trace_rays(const char* sph_sq, const double* sph_yoff, const double* sph_r, int n_sph,
-                   const char* light_sq, const double* light_col, int n_lights, const double* starts,
+int ref_trace_rays(const char* children, int n_children, const double* sph_yoff, const double* sph_r,
+                   const double* mesh_edge, const char* light_sq, const double* light_col, int n_lights,
+                   const double* starts,
                    const double* ends, int n, int depth, double* rgb) {
-    RefScene rs = build(sph_sq, sph_yoff, sph_r, n_sph, light_sq, light_col, n_lights);
+    RefScene rs = build(children, n_children, sph_yoff, sph_r, mesh_edge, light_sq, light_col, n_lights);
 #pragma omp parallel for schedule(dynamic, 64)
     for (int k = 0; k < n; ++k) {
         Point color(0.0, 0.0, 0.0);
@@ -117,23 +132,26 @@ int ref_trace_rays(const char* sph_sq, const double* sph_yoff, const double* sph
     return 0;
 }
 
-// g_scene.intersection(ray, Point(0,0,0), inter) on arbitrary rays: per ray 9 doubles
-// (point, normal, reflectedRay end) + hit flag + material id.
-int ref_intersect(const char* sph_sq, const double* sph_yoff, const double* sph_r, int n_sph,
-                  const double* starts, const double* ends, int n, double* out9, int32_t* hit,
-                  int32_t* mat) {
-    RefScene rs = build(sph_sq, sph_yoff, sph_r, n_sph, "", nullptr, 0);
+// g_scene.intersection(ray, Point(0,0,0), inter) on arbitrary rays: per ray 12 doubles
+// (point, normal, reflectedRay end, transmittedRay end) + hit flag + material id.
+int ref_intersect(const char* children, int n_children, const double* sph_yoff, const double* sph_r,
+                  const double* mesh_edge, const double* starts, const double* ends, int n, double* out12,
+                  int32_t* hit, int32_t* mat) {
+    RefScene rs = build(children, n_children, sph_yoff, sph_r, mesh_edge, "", nullptr, 0);
     for (int k = 0; k < n; ++k) {
         Intersection in;
         rs.scene->intersection(Line(Point(starts + 3 * k), Point(ends + 3 * k)), Point(0.0, 0.0, 0.0), in);
         hit[k] = in.intersects() ? 1 : 0;
         mat[k] = -1;
-        for (int q = 0; q < 9; ++q) out9[9 * k + q] = 0.0;
+        for (int q = 0; q < 12; ++q) out12[12 * k + q] = 0.0;
         if (hit[k]) {
             Point p = in.point(), nn = in.normal(), e = in.reflectedRay().endPoint();
-            out9[9 * k + 0] = p.x(); out9[9 * k + 1] = p.y(); out9[9 * k + 2] = p.z();
-            out9[9 * k + 3] = nn.x(); out9[9 * k + 4] = nn.y(); out9[9 * k + 5] = nn.z();
-            out9[9 * k + 6] = e.x(); out9[9 * k + 7] = e.y(); out9[9 * k + 8] = e.z();
+            Point t = in.transmittedRay().endPoint();
+            double* o = out12 + 12 * k;
+            o[0] = p.x(); o[1] = p.y(); o[2] = p.z();
+            o[3] = nn.x(); o[4] = nn.y(); o[5] = nn.z();
+            o[6] = e.x(); o[7] = e.y(); o[8] = e.z();
+            o[9] = t.x(); o[10] = t.y(); o[11] = t.z();
             mat[k] = material_id(in.material());
         }
     }

@@ -12,6 +12,7 @@
  *   Shape::intersection        :724-823      (bounding sphere, sphere, composite closest hit)
  *   Quad                       :826-843      (2 triangles, first hit wins)
  *   CheckerBoard::intersection :1084-1113
+ *   Tetrahedron ctor           :863-900      Cube ctor :903-950 (composite Shapes of Triangles / Quads)
  *   attenuation                :1171-1182    rayTraceRay :1184-1249 (recursive, as the reference)
  *   rayTraceScreen basis       :1270-1279    convertStringCoordinate :1326-1346
  * The structure deliberately follows the reference (recursion, composite walk, closest hit for shadow
@@ -138,6 +139,20 @@ typedef struct {
     Mat mat;
 } Sph;
 
+/* A composite Shape of the reference (Tetrahedron / Cube): bounding sphere, then sub-objects.
+ * Tetrahedron sub-objects are Triangles; Cube sub-objects are Quads (2 triangles, first hit wins). */
+typedef struct {
+    int kind;         /* RT_MESH_TETRAHEDRON / RT_MESH_CUBE */
+    P pos;            /* Shape _position (scene-local p) */
+    double radius;    /* sqrt(3)*edge/2 */
+    int mat_id;       /* 3 tetrahedron, 4 cube */
+    int nfaces;
+    int ntri[6];      /* 1 (triangle) or 2 (quad) */
+    Tri tri[6][2];
+} Mesh;
+
+typedef struct { int type; int index; } Child;   /* type: 0 board, 1 sphere, 2 mesh */
+
 typedef struct {
     P position;       /* g_scene _position */
     double radius;    /* g_scene _radius (bounding sphere) */
@@ -151,7 +166,47 @@ typedef struct {
     Sph* sph;
     int n_lights;
     P lcol[RT_MAX_LIGHTS], lpos[RT_MAX_LIGHTS];
+    int n_mesh;
+    Mesh* mesh;
+    Mat mesh_mat[3];  /* [1] tetrahedron, [2] cube */
+    int n_child;
+    Child* child;     /* g_scene _subObjects order */
 } Scene;
+
+static void mesh_build(Mesh* m, const rt_mesh* d, Mat mat, int mat_id, double eps) {  /* :863-950 */
+    P zero = pt(0.0, 0.0, 0.0);
+    double h = d->edge / 2;
+    m->kind = d->kind;
+    m->pos = from3(d->position);
+    m->radius = sqrt((double)3) * d->edge / 2;
+    m->mat_id = mat_id;
+    if (d->kind == RT_MESH_TETRAHEDRON) {
+        P v[4][3] = {
+            {pt(-h, -h, -h), pt(h, -h, -h), pt(-h, -h, h)},     /* bottom */
+            {pt(-h, -h, -h), pt(-h, -h, h), pt(-h, h, -h)},     /* back */
+            {pt(-h, -h, -h), pt(-h, h, -h), pt(-h, -h, h)},     /* left */
+            {pt(-h, -h, h), pt(h, -h, -h), pt(-h, h, -h)}};     /* front */
+        m->nfaces = 4;
+        for (int f = 0; f < 4; ++f) {
+            m->ntri[f] = 1;
+            tri_init(&m->tri[f][0], zero, mat, v[f][0], v[f][1], v[f][2], eps);
+        }
+    } else {
+        P q[6][4] = {
+            {pt(-h, h, -h), pt(h, h, -h), pt(h, h, h), pt(-h, h, h)},       /* top */
+            {pt(-h, -h, -h), pt(h, -h, -h), pt(h, -h, h), pt(-h, -h, h)},   /* bottom */
+            {pt(-h, -h, -h), pt(-h, h, -h), pt(-h, h, h), pt(-h, -h, h)},   /* left */
+            {pt(h, -h, -h), pt(h, h, -h), pt(h, h, h), pt(h, -h, h)},       /* right */
+            {pt(-h, -h, -h), pt(h, -h, -h), pt(h, h, -h), pt(-h, h, -h)},   /* back */
+            {pt(-h, -h, h), pt(h, -h, h), pt(h, h, h), pt(-h, h, h)}};      /* front */
+        m->nfaces = 6;
+        for (int f = 0; f < 6; ++f) {                           /* Quad(zero, m, p1..p4) (:826-843) */
+            m->ntri[f] = 2;
+            tri_init(&m->tri[f][0], zero, mat, q[f][0], q[f][1], q[f][2], eps);
+            tri_init(&m->tri[f][1], zero, mat, q[f][0], q[f][2], q[f][3], eps);
+        }
+    }
+}
 
 static int scene_build(const rt_scene* d, Scene* s) {
     memset(s, 0, sizeof(*s));
@@ -190,10 +245,37 @@ static int scene_build(const rt_scene* d, Scene* s) {
         s->lcol[k] = from3(d->lights[k].color);
         s->lpos[k] = from3(d->lights[k].position);
     }
+    if (d->n_meshes < 0 || d->n_meshes > RT_MAX_MESHES || (d->n_meshes > 0 && !d->meshes)) return RT_EINVAL;
+    s->mesh_mat[1] = mat_from(&d->tetrahedron_material);
+    s->mesh_mat[2] = mat_from(&d->cube_material);
+    s->n_mesh = d->n_meshes;
+    s->mesh = (Mesh*)calloc((size_t)(d->n_meshes > 0 ? d->n_meshes : 1), sizeof(Mesh));
+    s->child = (Child*)calloc((size_t)(1 + d->n_spheres + d->n_meshes), sizeof(Child));
+    if (!s->mesh || !s->child) return RT_ENOMEM;
+    for (int m = 0; m < d->n_meshes; ++m) {
+        int kind = d->meshes[m].kind;
+        if (kind != RT_MESH_TETRAHEDRON && kind != RT_MESH_CUBE) return RT_EINVAL;
+        mesh_build(&s->mesh[m], &d->meshes[m], s->mesh_mat[kind], kind == RT_MESH_TETRAHEDRON ? 3 : 4, s->eps);
+    }
+    /* g_scene child order: board, then spheres with each mesh inserted after `after_spheres` spheres */
+    int nc = 0, m = 0;
+    if (s->has_board) { s->child[nc].type = 0; s->child[nc].index = 0; ++nc; }
+    for (int k = 0; k <= d->n_spheres; ++k) {
+        while (m < d->n_meshes && d->meshes[m].after_spheres <= k) {
+            s->child[nc].type = 2; s->child[nc].index = m; ++nc; ++m;
+        }
+        if (k < d->n_spheres) { s->child[nc].type = 1; s->child[nc].index = k; ++nc; }
+    }
+    while (m < d->n_meshes) { s->child[nc].type = 2; s->child[nc].index = m; ++nc; ++m; }
+    s->n_child = nc;
     return RT_OK;
 }
 
-static void scene_free(Scene* s) { free(s->sph); s->sph = NULL; }
+static void scene_free(Scene* s) {
+    free(s->sph); s->sph = NULL;
+    free(s->mesh); s->mesh = NULL;
+    free(s->child); s->child = NULL;
+}
 
 /* Quad = Shape(p, m, 0, false, true): no bound test (radius 0), first hit returns (:817). */
 static void quad_intersect(const Scene* s, Line ray, P off, Inter* in) {
@@ -251,6 +333,45 @@ static void sphere_intersect(const Sph* sp, Line ray, P off, double eps, Inter* 
     in->trans.s = p; in->trans.e = add(p, tv);
 }
 
+/* Tetrahedron / Cube: Shape::intersection with radius > 0, not a sphere (:736-823): bounding-sphere
+ * cull, then the closest sub-object (strict <); a Cube's sub-objects are Quads (first hit, :817). */
+static void mesh_intersect(const Mesh* me, Line ray, P off, double eps, Inter* in) {
+    P u = line_dir(ray);
+    P p0 = ray.s;
+    P position = add(me->pos, off);
+    P deltaP = sub(position, p0);
+    if (me->radius > 0) {
+        double uDeltaP = dot(u, deltaP);
+        double disc = uDeltaP * uDeltaP - dot(deltaP, deltaP) + me->radius * me->radius;
+        double sv = uDeltaP - sqrt(disc);
+        if (disc < 0 || fabs(sv) < eps) { in->hit = 0; return; }
+    }
+    in->hit = 0;
+    double minDistance = -1.0;
+    for (int f = 0; f < me->nfaces; ++f) {
+        Inter tmp;
+        tmp.hit = 0;
+        if (me->ntri[f] == 1) {
+            tri_intersect(&me->tri[f][0], ray, position, eps, &tmp);
+        } else {                                   /* Quad(zero, ...): position = zero + offset */
+            P qpos = add(pt(0.0, 0.0, 0.0), position);
+            for (int t = 0; t < 2 && !tmp.hit; ++t) {
+                Inter tt;
+                tri_intersect(&me->tri[f][t], ray, qpos, eps, &tt);
+                if (tt.hit) tmp = tt;              /* first hit wins */
+            }
+        }
+        if (tmp.hit) {
+            double d = len(sub(tmp.point, p0));
+            if (d < minDistance || minDistance < 0.0) {
+                minDistance = d;
+                *in = tmp;
+                in->mat_id = me->mat_id;
+            }
+        }
+    }
+}
+
 /* g_scene.intersection(ray, Point(0,0,0), inter): bounding sphere then closest child (:724-823). */
 static void scene_intersect(const Scene* s, Line ray, Inter* in) {
     P off = pt(0.0, 0.0, 0.0);
@@ -266,11 +387,12 @@ static void scene_intersect(const Scene* s, Line ray, Inter* in) {
     }
     in->hit = 0;
     double minDistance = -1.0;
-    int nchild = s->has_board + s->n_sph;
-    for (int c = 0; c < nchild; ++c) {
+    for (int c = 0; c < s->n_child; ++c) {
         Inter tmp;
-        if (s->has_board && c == 0) board_intersect(s, ray, position, &tmp);
-        else sphere_intersect(&s->sph[c - s->has_board], ray, position, s->eps, &tmp);
+        const Child ch = s->child[c];
+        if (ch.type == 0) board_intersect(s, ray, position, &tmp);
+        else if (ch.type == 1) sphere_intersect(&s->sph[ch.index], ray, position, s->eps, &tmp);
+        else mesh_intersect(&s->mesh[ch.index], ray, position, s->eps, &tmp);
         if (tmp.hit) {
             double d = len(sub(tmp.point, p0));
             if (d < minDistance || minDistance < 0.0) {
@@ -429,6 +551,8 @@ int oracle_intersect(const rt_scene* d, const double* starts, const double* ends
             h->normal[0] = in.normal.x; h->normal[1] = in.normal.y; h->normal[2] = in.normal.z;
             h->reflected_end[0] = in.refl.e.x; h->reflected_end[1] = in.refl.e.y;
             h->reflected_end[2] = in.refl.e.z;
+            h->transmitted_end[0] = in.trans.e.x; h->transmitted_end[1] = in.trans.e.y;
+            h->transmitted_end[2] = in.trans.e.z;
         }
     }
     scene_free(&s);

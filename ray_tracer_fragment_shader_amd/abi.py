@@ -21,7 +21,10 @@ RT_ENOMEM = -3
 RT_EUNSUPPORTED = -4
 RT_MAX_SPHERES = 1024
 RT_MAX_LIGHTS = 16
+RT_MAX_MESHES = 64
 RT_MAX_DEPTH = 7
+RT_MESH_TETRAHEDRON = 1
+RT_MESH_CUBE = 2
 
 D3 = c_double * 3
 
@@ -36,6 +39,10 @@ class rt_sphere(Structure):
 
 class rt_light(Structure):
     _fields_ = [("color", D3), ("position", D3)]
+
+
+class rt_mesh(Structure):
+    _fields_ = [("kind", c_int32), ("after_spheres", c_int32), ("position", D3), ("edge", c_double)]
 
 
 class rt_scene(Structure):
@@ -56,6 +63,11 @@ class rt_scene(Structure):
         ("sphere_material", rt_material),
         ("spheres", POINTER(rt_sphere)),
         ("lights", POINTER(rt_light)),
+        ("tetrahedron_material", rt_material),
+        ("cube_material", rt_material),
+        ("n_meshes", c_int32),
+        ("reserved1", c_int32),
+        ("meshes", POINTER(rt_mesh)),
     ]
 
 
@@ -74,7 +86,8 @@ class rt_stats(Structure):
 
 
 class rt_hit(Structure):
-    _fields_ = [("point", D3), ("normal", D3), ("reflected_end", D3), ("hit", c_int32), ("material", c_int32)]
+    _fields_ = [("point", D3), ("normal", D3), ("reflected_end", D3), ("transmitted_end", D3), ("hit", c_int32),
+                ("material", c_int32)]
 
 
 class RtError(RuntimeError):
@@ -94,7 +107,8 @@ SIGNATURES = {
     "rt_scene_init_reference": (c_int, [_P(rt_scene)]),
     "rt_convert_string_coordinate": (c_int, [c_char_p, _P(c_double)]),
     "rt_light_position_from_square": (c_int, [c_char_p, _P(c_double)]),
-    "rt_load_scene": (c_int, [_P(c_char_p), _P(c_int32), c_int, _P(rt_scene), _P(rt_sphere), c_int, _P(rt_light)]),
+    "rt_load_scene": (c_int, [_P(c_char_p), _P(c_int32), c_int, _P(rt_scene), _P(rt_sphere), c_int, _P(rt_mesh),
+                              c_int, _P(rt_light)]),
     "rt_camera_init_reference": (c_int, [_P(rt_camera), c_int, c_int, c_double]),
     "rt_local_rows": (c_int, [c_int, _P(rt_rows), _P(c_int)]),
     "rt_global_row": (c_int, [c_int, _P(rt_rows), c_int, _P(c_int)]),
@@ -124,7 +138,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.rt_abi_version() != 1:
+        if L.rt_abi_version() != 2:
             raise RuntimeError("librt_amd.so ABI version mismatch")
         _lib = L
     return _lib

@@ -7,6 +7,7 @@
 // the image goes to a PPM file (the output path the reference already has).
 //
 //   rt_render --config c2 --out c2.ppm            canonical scene
+//   rt_render --config demo --out demo.ppm        initScene's demo (tetrahedron, sphere, cube), 500x500
 //   rt_render --stdin --width 500 --height 500 --pitch 1 --out app.ppm < answers.txt
 //                                                  initScene2's questions answered on stdin
 #include <cmath>
@@ -101,12 +102,13 @@ int main(int argc, char** argv) {
         else if (a == "--depth") o.depth = std::atoi(next().c_str());
         else if (a == "--pitch") o.pitch = std::atof(next().c_str());
         else if (a == "--device") o.device = std::atoi(next().c_str());
-        else { std::fprintf(stderr, "usage: rt_render [--config c1|c2|c3|c5 | --stdin] [--width W --height H "
+        else { std::fprintf(stderr, "usage: rt_render [--config c1|c2|c3|c5|demo | --stdin] [--width W --height H "
                                     "--pitch P --depth B] [--device N] [--out file.ppm]\n"); return 2; }
     }
 
     rt_scene scene;
     std::vector<rt_sphere> spheres(RT_MAX_SPHERES);
+    std::vector<rt_mesh> meshes(RT_MAX_MESHES);
     std::vector<rt_light> lights(2);
     int W, H, depth;
     double pitch;
@@ -117,12 +119,34 @@ int main(int argc, char** argv) {
         std::vector<const char*> csq;
         for (auto& s : sq) csq.push_back(s.c_str());
         check(rt_load_scene(csq.data(), ty.data(), (int)csq.size(), &scene, spheres.data(), RT_MAX_SPHERES,
-                            &lights[0]),
+                            meshes.data(), RT_MAX_MESHES, &lights[0]),
               "rt_load_scene");
         W = o.width > 0 ? o.width : 500;                    // g_windowWidth/Height (:570)
         H = o.height > 0 ? o.height : 500;
         depth = o.depth >= 0 ? o.depth : 5;                 // MAX_DEPTH (:48)
         pitch = o.pitch > 0 ? o.pitch : 1.0;                // rayTraceScreen's unit pixel step
+    } else if (o.config == "demo") {
+        // initScene (MySdlApplication.cpp:1387-1428): light b6, tetrahedron b4, sphere d7 (r 20),
+        // cube a7, inserted in that order after the board; the app's 500x500 window, MAX_DEPTH 5.
+        check(rt_scene_init_reference(&scene), "rt_scene_init_reference");
+        check(rt_convert_string_coordinate("d7", spheres[0].center), "rt_convert_string_coordinate");
+        spheres[0].radius = 20.0;
+        meshes[0] = rt_mesh{RT_MESH_TETRAHEDRON, 0, {0, 0, 0}, 40.0};
+        meshes[1] = rt_mesh{RT_MESH_CUBE, 1, {0, 0, 0}, 40.0};
+        check(rt_convert_string_coordinate("b4", meshes[0].position), "rt_convert_string_coordinate");
+        check(rt_convert_string_coordinate("a7", meshes[1].position), "rt_convert_string_coordinate");
+        check(rt_light_position_from_square("b6", lights[0].position), "rt_light_position_from_square");
+        for (int q = 0; q < 3; ++q) lights[0].color[q] = 1.0;
+        scene.n_spheres = 1;
+        scene.spheres = spheres.data();
+        scene.n_meshes = 2;
+        scene.meshes = meshes.data();
+        scene.n_lights = 1;
+        scene.lights = lights.data();
+        W = o.width > 0 ? o.width : 500;
+        H = o.height > 0 ? o.height : 500;
+        depth = o.depth >= 0 ? o.depth : 5;
+        pitch = o.pitch > 0 ? o.pitch : 1.0;
     } else {
         Canonical c = canonical(o.config);
         check(rt_scene_init_reference(&scene), "rt_scene_init_reference");

@@ -55,8 +55,11 @@ struct SceneView {
     const DevSpherePrim* prim;
     const DevSphereF* sphf;
     const DevSpherePrimF* primf;
+    const DevMesh* mesh;             // global, wave-uniform reads
+    const DevTri* tri;
     int np;                          // padded sphere count (wave-uniform)
     int nl;                          // light count (wave-uniform)
+    int nm;                          // mesh count (wave-uniform)
 };
 
 // hdr: header copy the kernel reads (LDS or global); g: the global record (for the filter images).
@@ -71,8 +74,14 @@ __device__ __forceinline__ SceneView view_of(const DevScene* hdr, const DevScene
     const DevSpherePrim* gprim = reinterpret_cast<const DevSpherePrim*>(gsph + np);
     v.sphf = reinterpret_cast<const DevSphereF*>(gprim + np);
     v.primf = reinterpret_cast<const DevSpherePrimF*>(v.sphf + np);
+    v.mesh = reinterpret_cast<const DevMesh*>(v.primf + np);
+    v.nm = g->n_meshes;
+    v.tri = reinterpret_cast<const DevTri*>(v.mesh + v.nm);
     return v;
 }
+
+// Hit kinds: -1 miss, 0 board, 1 + k sphere k, kMeshKind + 16 m + t mesh m's triangle t.
+constexpr int kMeshKind = 1 << 20;
 
 // A ray Line(p0, p0 + d) with u = normalize(d), plus its FP32 filter image.
 struct Ray {
@@ -155,6 +164,102 @@ __device__ __forceinline__ bool board_hit(const DevScene* S, d3 p0, d3 d, d3* p)
     return false;
 }
 
+// Triangle::intersection (:611-707) on a mesh triangle, with the same division-skipping sign tests as
+// board_hit.  d = end - start (unnormalised).
+__device__ __forceinline__ bool tri_hit(const DevTri& T, d3 p0, d3 d, double eps, d3* p) {
+    if (T.degenerate != 0.0) return false;                  // :633-637
+    d3 n = ld3(T.n);
+    double nd = dot(n, d);                                  // :648
+    if (fabs(nd) < eps) return false;                       // :651
+    d3 v0 = ld3(T.v0);
+    double num = dot(n, sub(v0, p0));
+    if (num == 0.0 || ((num < 0.0) != (nd < 0.0))) return false;
+    double m = num / nd;                                    // :657
+    if (m < eps) return false;                              // :659
+    d3 q = add(p0, scl(m, d));                              // :665
+    d3 w = sub(q, v0);                                      // :667
+    double wu = dot(w, ld3(T.u));
+    double wv = dot(w, ld3(T.v));
+    double A = T.uv * wv - T.vv * wu;
+    double B = T.uv * wu - T.uu * wv;
+    if (A > T.thr || B > T.thr) return false;
+    double s = A / T.den;                                   // :673
+    double tt = B / T.den;                                  // :674
+    if (s >= 0 && tt >= 0 && s + tt <= 1) {                 // :676
+        *p = q;
+        return true;
+    }
+    return false;
+}
+
+// A mesh's own bounding-sphere cull (Shape::intersection with radius > 0, :747-758).
+__device__ __forceinline__ bool mesh_bound(const DevMesh& M, d3 p0, d3 u, double eps) {
+    d3 dP = sub(ld3(M.bc), p0);
+    double dd = dot(dP, dP);
+    if (dd < M.inner2) return true;
+    double uD = dot(u, dP);
+    double disc = uD * uD - dd + M.br2;
+    if (disc < 0) return false;
+    double s = uD - sqrt(disc);
+    return !(fabs(s) < eps);
+}
+
+// The mesh's closest sub-object hit (strict <, in sub-object order; a cube face is a Quad: its second
+// triangle is tested only if the first misses, :817).  Returns the triangle index or -1.
+__device__ __forceinline__ int mesh_closest_tri(const SceneView& V, const DevMesh& M, d3 p0, d3 d, double eps,
+                                                double* mbest, d3* mq) {
+    int mt = -1;
+    *mbest = -1.0;
+    for (int f = 0; f < M.nfaces; ++f) {
+        int t = M.tri0 + f * M.per_face;
+        d3 q;
+        bool h = tri_hit(V.tri[t], p0, d, eps, &q);
+        if (!h && M.per_face == 2) {
+            ++t;
+            h = tri_hit(V.tri[t], p0, d, eps, &q);
+        }
+        if (h) {
+            double dist = len(sub(q, p0));
+            if (dist < *mbest || *mbest < 0.0) {
+                *mbest = dist;
+                mt = t;
+                *mq = q;
+            }
+        }
+    }
+    return mt;
+}
+
+// Position of a hit kind in g_scene's child list (only evaluated on exact distance ties).
+__device__ __forceinline__ int child_of(const SceneView& V, int kind) {
+    const int hb = V.S->has_board ? 1 : 0;
+    if (kind == 0) return 0;
+    if (kind >= kMeshKind) return V.mesh[(kind - kMeshKind) >> 4].child;
+    const int k = kind - 1;
+    int before = 0;
+    for (int m = 0; m < V.nm; ++m) before += (V.mesh[m].child - hb - m) <= k ? 1 : 0;
+    return hb + k + before;
+}
+
+// Meshes after the board and the spheres: (distance, child index) order = the reference's ordered
+// strict-< walk over the child list.
+__device__ __forceinline__ void meshes_closest(const SceneView& V, const Ray& r, double eps, int* kind,
+                                               double* best, d3* hp) {
+    for (int m = 0; m < V.nm; ++m) {
+        const DevMesh& M = V.mesh[m];
+        if (!mesh_bound(M, r.p0, r.u, eps)) continue;
+        double mbest;
+        d3 mq;
+        int t = mesh_closest_tri(V, M, r.p0, r.d, eps, &mbest, &mq);
+        if (t < 0) continue;
+        if (mbest < *best || *best < 0.0 || (mbest == *best && M.child < child_of(V, *kind))) {
+            *best = mbest;
+            *kind = kMeshKind + 16 * m + (t - M.tri0);
+            *hp = mq;
+        }
+    }
+}
+
 // FP32 filter: true only if disc = uD^2 - |dP|^2 + r^2 < 0 is certain.
 // Error budget (eps32 = 2^-24; S >= |c_i| + |p_i| per component, c, p relative to the bound centre):
 // |d(dx)| <= 2 eps32 S; |d(uD)| <= 10.4 eps32 S; |d(uD^2)| <= 36 eps32 S^2; |d(dd)| <= 21 eps32 S^2;
@@ -214,6 +319,7 @@ __device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const R
     }
 }
 
+template <bool FULL>
 __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3* hp) {
     const DevScene* S = V.S;
     if (!bound_pass(S, r.p0, r.u)) return -1;
@@ -229,11 +335,13 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
     }
     const double eps = S->eps;
     for (int k0 = 0; k0 < V.np; k0 += kChunk) sphere_batch_closest(V, r, k0, eps, &kind, &best, hp);
+    if (FULL) meshes_closest(V, r, eps, &kind, &best, hp);
     return kind;
 }
 
 // Closest hit of a primary ray Line(eye, sp): deltaP and |deltaP|^2 per sphere were computed for this
 // eye by rt_prepare_kernel with the reference's operations (:740, :750).
+template <bool FULL>
 __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray& r, d3 bdP, double bdd,
                                                    d3* hp) {
     const DevScene* S = V.S;
@@ -274,10 +382,12 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
             }
         }
     }
+    if (FULL) meshes_closest(V, r, eps, &kind, &best, hp);
     return kind;
 }
 
 // Shadow test: intersects() of g_scene.intersection(Line(pt, Lpos)) (:1216-1221), any hit.
+template <bool FULL>
 __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r) {
     const DevScene* S = V.S;
     if (!bound_pass(S, r.p0, r.u)) return false;
@@ -297,7 +407,49 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r) {
         d3 q;
         if (board_hit(S, r.p0, r.d, &q)) return true;
     }
+    for (int m = 0; FULL && m < V.nm; ++m) {
+        const DevMesh& M = V.mesh[m];
+        if (!mesh_bound(M, r.p0, r.u, eps)) continue;
+        for (int t = M.tri0; t < M.tri0 + M.nfaces * M.per_face; ++t) {
+            d3 q;
+            if (tri_hit(V.tri[t], r.p0, r.d, eps, &q)) return true;
+        }
+    }
     return false;
+}
+
+// Material of a hit (checker parity for the board, :1101-1111).
+__device__ __forceinline__ int material_of(const SceneView& V, int kind, d3 p) {
+    const DevScene* S = V.S;
+    if (kind == 0) {
+        d3 q = add(sub(p, ld3(S->coff)), mk(S->half, 0.0, S->half));
+        int squareSum = (int)(q.x / S->square) + (int)(q.z / S->square);
+        return (squareSum & 1) == 0 ? 0 : 1;
+    }
+    if (kind >= kMeshKind) return V.mesh[(kind - kMeshKind) >> 4].mat;
+    return 2;
+}
+
+// Shadow test when some material is transparent: the closest blocker decides (:1219-1221).
+__device__ __forceinline__ bool occluded_transparent(const SceneView& V, const Ray& r) {
+    d3 p;
+    int kind = closest_hit<true>(V, r, &p);
+    if (kind < 0) return false;
+    return V.S->mat[material_of(V, kind, p)].transparent == 0;
+}
+
+// Transmitted ray end p + t (:685-699, :780-791) with the refraction of the object's own material: the
+// board's triangles carry Material() (refraction 1, :291-293, :838-841), spheres and meshes theirs.
+__device__ __forceinline__ d3 transmitted_end(const SceneView& V, int kind, int mat, d3 p, d3 u, d3 n) {
+    double rr = kind == 0 ? 1.0 : V.S->mat[mat].refr;
+    d3 t = mk(0.0, 0.0, 0.0);
+    double cti = dot(u, n);                                 // :690
+    double modulus = 1 - rr * rr * (1 - cti * cti);         // :691
+    if (modulus > 0) {
+        double ctr = sqrt(modulus);
+        t = sub(scl(rr, u), scl(ctr + rr * cti, n));        // :696
+    }
+    return add(p, t);                                       // Line(p, p + t) (:699)
 }
 
 // Surface data of a hit: normal, material id, reflected end point p + r (:679-683, :774-778, :1101-1111).
@@ -305,21 +457,23 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
     const DevScene* S = V.S;
     if (kind == 0) {
         *n = ld3(S->tri[0].n);
-        d3 q = add(sub(p, ld3(S->coff)), mk(S->half, 0.0, S->half));
-        int squareSum = (int)(q.x / S->square) + (int)(q.z / S->square);
-        *mat = (squareSum & 1) == 0 ? 0 : 1;
+    } else if (kind >= kMeshKind) {
+        const DevMesh& M = V.mesh[(kind - kMeshKind) >> 4];
+        *n = ld3(V.tri[M.tri0 + ((kind - kMeshKind) & 15)].n);
     } else {
         d3 c = ld3(V.sph[kind - 1].c);
         d3 dp = sub(p, c);                                  // directionP0 (:763)
         *n = divs(dp, len(dp));                             // :774-775
-        *mat = 2;
     }
+    *mat = material_of(V, kind, p);
     d3 r = sub(u, scl(2 * dot(u, *n), *n));                 // :682 / :777
     *pe = add(p, r);                                        // Line(p, p + r)
 }
 
 // Local illumination of one hit over all lights (:1213-1228).  u = incoming ray direction,
 // rdir = reflectedRay().direction().
+// FULL: meshes may be present and materials may be transparent (closest-hit shadows, :1219-1221).
+template <bool FULL>
 __device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 u, d3 rdir) {
     const DevScene* S = V.S;
     const DevMat& M = S->mat[mat];
@@ -335,7 +489,7 @@ __device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 
         double dl = len(sd);                                // shadowRay.length()
         d3 sdir = divs(sd, dl);                             // shadowRay.direction()
         set_dir(&sr, sd, sdir);
-        if (!occluded(V, sr)) {
+        if (!(FULL ? occluded_transparent(V, sr) : occluded<false>(V, sr))) {
             double a = S->att / (S->att + dl * dl);         // attenuation (:1181)
             d3 lC = scl(a, ld3(S->light[i].col));           // :1223
             d3 term = add(add(had(amb, lC), scl(fabs(dot(n, sdir)), had(dif, lC))), scl(ks, had(spc, lC)));
@@ -346,13 +500,18 @@ __device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 
 }
 
 // rayTraceRay(g_scene, lights, Line(p0, p1), color, B) with color starting at 0 (:1184-1249), as a loop.
+// Every in-scope hit spawns exactly one continuation (host-checked): the reflected ray (opacity != 0) or
+// the transmitted ray (transparency != 0 and |transparency| > eps), weighted by that vector (:1238-1247),
+// so the colour is the right-nested local[0] + w[0] % (local[1] + w[1] % (...)).  TRANSP = false: all
+// materials opaque, no meshes, w = (1,1,1) (multiplication by 1.0 is exact) and any-hit shadows.
 // PRIMARY: p0 is the camera and V.prim/V.primf hold its per-sphere data; (bdP, bdd) = bc - eye, |.|^2.
 // seg / shadow count the rays actually traced.
-template <int B, bool PRIMARY>
+template <int B, bool PRIMARY, bool TRANSP>
 __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, double bdd, uint32_t* seg,
                                     uint32_t* shadow) {
     const DevScene* S = V.S;
     d3 local[B + 1];
+    d3 wgt[TRANSP ? B + 1 : 1];
     int levels = 0;
     Ray r;
     r.p0 = p0;
@@ -362,6 +521,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
 #pragma unroll
     for (int lvl = 0; lvl <= B; ++lvl) {
         local[lvl] = mk(0.0, 0.0, 0.0);
+        if (TRANSP) wgt[lvl] = mk(1.0, 1.0, 1.0);
         bool alive = lvl == 0 || levels == lvl;
         if (!__any(alive)) break;                           // the whole wave has missed: early out
         if (alive) {
@@ -369,10 +529,10 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
             d3 p;
             int kind;
             if (PRIMARY && lvl == 0) {
-                kind = closest_hit_primary(V, r, bdP, bdd, &p);
+                kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, &p);
             } else {
                 set_origin_f32(S, &r);
-                kind = closest_hit(V, r, &p);
+                kind = closest_hit<TRANSP>(V, r, &p);
             }
             if (kind >= 0) {
                 d3 n, pe;
@@ -380,18 +540,28 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                 surface(V, kind, p, r.u, &n, &mat, &pe);
                 d3 rd = sub(pe, p);                         // reflectedRay = Line(p, p + r)
                 d3 rdir = divs(rd, len(rd));                // reflectedRay.direction()
-                local[lvl] = shade(V, p, n, mat, r.u, rdir);
+                local[lvl] = shade<TRANSP>(V, p, n, mat, r.u, rdir);
                 nsh += V.nl;
                 levels = lvl + 1;
-                r.p0 = p;                                   // next level traces the reflected ray
-                set_dir(&r, rd, rdir);
+                r.p0 = p;                                   // the next level traces the continuation
+                if (TRANSP && S->mat[mat].transmit) {
+                    d3 pt = transmitted_end(V, kind, mat, p, r.u, n);
+                    d3 td = sub(pt, p);                     // transmittedRay = Line(p, p + t)
+                    set_dir(&r, td, divs(td, len(td)));
+                } else {
+                    set_dir(&r, rd, rdir);
+                }
+                if (TRANSP) wgt[lvl] = ld3(S->mat[mat].w);
             }
         }
     }
     d3 acc = mk(0.0, 0.0, 0.0);
 #pragma unroll
     for (int lvl = B; lvl >= 0; --lvl) {
-        if (lvl < levels) acc = (lvl == levels - 1) ? local[lvl] : add(local[lvl], acc);
+        if (lvl < levels) {
+            if (lvl == levels - 1) acc = local[lvl];
+            else acc = TRANSP ? add(local[lvl], had(wgt[lvl], acc)) : add(local[lvl], acc);
+        }
     }
     *seg = nseg;
     *shadow = nsh;

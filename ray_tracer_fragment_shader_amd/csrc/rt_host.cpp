@@ -3,6 +3,7 @@
 //
 // Citations are into /root/reference/Hw4/MySdlApplication.cpp unless a file is named.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -40,6 +41,7 @@ inline void put(double* d, HP a) { d[0] = a.x; d[1] = a.y; d[2] = a.z; }
 // Reference constants (:31-52).
 const double kWhite[3] = {1.0, 1.0, 1.0};
 const double kBlack[3] = {0.0, 0.0, 0.0};
+const double kRed[3] = {1.0, 0.0, 0.0};
 const double kBoardPosition[3] = {0, 0, -160};
 const double kBoardEdge = 320.0;
 const double kBoardHalf = kBoardEdge / 2;
@@ -88,6 +90,9 @@ extern "C" int rt_scene_init_reference(rt_scene* s) {
     set_material(&s->white_square, .1 * white, .5 * white, white, black, 1);    // :583
     set_material(&s->black_square, black, .1 * white, black, black, 1);         // :585
     set_material(&s->sphere_material, black, .1 * white, white, black, 1);      // :586
+    set_material(&s->tetrahedron_material, black, black, .1 * white, white, 2.0 / 3.0);  // :587
+    HP red = hp(kRed);
+    set_material(&s->cube_material, .1 * red, .4 * red, red, black, 1);         // :588
     return RT_OK;
 }
 
@@ -110,7 +115,7 @@ extern "C" int rt_light_position_from_square(const char* sq, double out[3]) {  /
 }
 
 extern "C" int rt_load_scene(const char* const* squares, const int32_t* types, int n, rt_scene* scene,
-                             rt_sphere* sphere_buf, int sphere_cap, rt_light* light) {
+                             rt_sphere* sphere_buf, int sphere_cap, rt_mesh* mesh_buf, int mesh_cap, rt_light* light) {
     if (!scene || n < 0 || (n > 0 && (!squares || !types))) return rt_fail(RT_EINVAL, "rt_load_scene: bad args");
     std::map<std::string, int> board_map;                                       // boardMap (:595)
     for (int k = 0; k < n; ++k) {
@@ -119,32 +124,41 @@ extern "C" int rt_load_scene(const char* const* squares, const int32_t* types, i
         board_map[std::string(squares[k])] = types[k];                          // :1467
     }
     rt_scene_init_reference(scene);
-    int ns = 0;
+    int ns = 0, nm = 0;
     bool unsupported = false;
-    bool have_light = false;
     double lpos[3] = {0.0, 0.0, 0.0};                                           // g_lightPosition (:573)
     for (const auto& kv : board_map) {                                          // :1503-1538
         const char* sq = kv.first.c_str();
         switch (kv.second) {
-            case 0:                                                             // LIGHT
+            case 0:                                                             // LIGHT (:1510-1513)
                 rt_light_position_from_square(sq, lpos);
-                have_light = true;
                 break;
-            case 3: {                                                           // SPHERE (:1521-1525)
+            case 1:                                                             // TETRAHEDRON (:1514-1517)
+            case 2: {                                                           // CUBE (:1518-1522)
+                if (nm >= mesh_cap || !mesh_buf) return rt_fail(RT_EINVAL, "rt_load_scene: mesh_buf too small");
+                rt_mesh& m = mesh_buf[nm++];
+                m.kind = kv.second == 1 ? RT_MESH_TETRAHEDRON : RT_MESH_CUBE;
+                m.after_spheres = ns;
+                rt_convert_string_coordinate(sq, m.position);
+                m.edge = kSquareEdge;
+                break;
+            }
+            case 3: {                                                           // SPHERE (:1523-1527)
                 if (ns >= sphere_cap || !sphere_buf) return rt_fail(RT_EINVAL, "rt_load_scene: sphere_buf too small");
                 rt_convert_string_coordinate(sq, sphere_buf[ns].center);
                 sphere_buf[ns].radius = kSquareEdge / 2;
                 ++ns;
                 break;
             }
-            default:                                                            // meshes: outside the GPU path
+            default:                                                            // CYLINDER / CONE: stubs
                 unsupported = true;
                 break;
         }
     }
-    (void)have_light;
     scene->n_spheres = ns;
     scene->spheres = sphere_buf;
+    scene->n_meshes = nm;
+    scene->meshes = mesh_buf;
     if (light) {
         put(light->color, hp(kWhite));                                          // g_lightColor (:577)
         put(light->position, hp(lpos));
@@ -152,7 +166,8 @@ extern "C" int rt_load_scene(const char* const* squares, const int32_t* types, i
         scene->lights = light;
     }
     if (unsupported)
-        return rt_fail(RT_EUNSUPPORTED, "rt_load_scene: tetrahedron/cube/cylinder/cone are outside the GPU path");
+        return rt_fail(RT_EUNSUPPORTED,
+                       "rt_load_scene: cylinder/cone are stubs in the reference (MySdlApplication.cpp:1000-1020, 457-458)");
     return RT_OK;
 }
 
@@ -220,13 +235,48 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     if (s->n_lights > 0 && !s->lights) return rt_fail(RT_EINVAL, "rt_set_scene: null lights");
     if (!(s->small_number >= 0) || !(s->square_edge_size != 0))
         return rt_fail(RT_EINVAL, "rt_set_scene: bad constants");
-    const rt_material* mats[3] = {&s->white_square, &s->black_square, &s->sphere_material};
-    for (const rt_material* m : mats)
-        if (!all_zero(m->transparency))
-            return rt_fail(RT_EUNSUPPORTED,
-                           "rt_set_scene: transparent materials (transmitted rays) are outside the GPU path");
+    if (s->n_meshes < 0 || s->n_meshes > RT_MAX_MESHES || (s->n_meshes > 0 && !s->meshes))
+        return rt_fail(RT_EINVAL, "rt_set_scene: bad meshes");
+    int n_tris = 0;
+    for (int m = 0; m < s->n_meshes; ++m) {
+        const rt_mesh& M = s->meshes[m];
+        if (M.kind != RT_MESH_TETRAHEDRON && M.kind != RT_MESH_CUBE) return rt_fail(RT_EINVAL, "rt_set_scene: bad mesh kind");
+        if (M.after_spheres < 0 || M.after_spheres > s->n_spheres || (m > 0 && M.after_spheres < s->meshes[m - 1].after_spheres))
+            return rt_fail(RT_EINVAL, "rt_set_scene: mesh after_spheres must be non-decreasing in [0, n_spheres]");
+        n_tris += M.kind == RT_MESH_TETRAHEDRON ? 4 : 12;
+    }
+    const rt_material* mats[5] = {&s->white_square, &s->black_square, &s->sphere_material, &s->tetrahedron_material,
+                                  &s->cube_material};
+    // rayTraceRay (:1230-1247) spawns a transmitted ray when transparency != 0 and |transparency| > eps, a
+    // reflected ray when opacity = 1 - transparency != 0.  The GPU loop follows one continuation per hit.
+    bool used[5] = {true, true, s->n_spheres > 0, false, false};
+    for (int m = 0; m < s->n_meshes; ++m) used[s->meshes[m].kind == RT_MESH_TETRAHEDRON ? 3 : 4] = true;
+    bool any_transparent = false;
+    rt::DevMat dm[5];
+    memset(dm, 0, sizeof(dm));
+    for (int m = 0; m < 5; ++m) {
+        const rt_material* M = mats[m];
+        HP T = hp(M->transparency);
+        HP opacity = hp(1.0, 1.0, 1.0) - T;                                     // :1236
+        bool zeroT = T.x == 0 && T.y == 0 && T.z == 0;
+        bool transmit = !zeroT && length(T) > s->small_number;                  // :1238
+        bool reflect = !(opacity.x == 0 && opacity.y == 0 && opacity.z == 0);   // :1243
+        if (used[m] && transmit && reflect)
+            return rt_fail(RT_EUNSUPPORTED, "rt_set_scene: a partially transparent material spawns two rays per hit "
+                                            "(a ray tree); the GPU path follows one continuation per hit");
+        if (used[m] && !zeroT) any_transparent = true;
+        for (int q = 0; q < 3; ++q) {
+            dm[m].amb[q] = M->ambient[q];
+            dm[m].diff[q] = M->diffuse[q];
+            dm[m].spec[q] = M->specular[q];
+        }
+        put(dm[m].w, transmit ? T : opacity);
+        dm[m].refr = M->refraction;
+        dm[m].transmit = transmit ? 1 : 0;
+        dm[m].transparent = zeroT ? 0 : 1;
+    }
 
-    const size_t bytes = (size_t)rt::scene_bytes_for(s->n_spheres);
+    const size_t bytes = (size_t)rt::scene_bytes_for(s->n_spheres, s->n_meshes, n_tris);
     const int np = rt::padded_spheres(s->n_spheres);
     blob->assign(bytes, 0);
     rt::DevScene* d = reinterpret_cast<rt::DevScene*>(blob->data());
@@ -296,13 +346,8 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
             return rt_fail(RT_EUNSUPPORTED, "rt_set_scene: half-degenerate board");
         }
     }
-    for (int m = 0; m < 3; ++m) {
-        for (int q = 0; q < 3; ++q) {
-            d->mat[m].amb[q] = mats[m]->ambient[q];
-            d->mat[m].diff[q] = mats[m]->diffuse[q];
-            d->mat[m].spec[q] = mats[m]->specular[q];
-        }
-    }
+    for (int m = 0; m < 5; ++m) d->mat[m] = dm[m];
+    d->transparent = any_transparent ? 1 : 0;
     d->n_lights = s->n_lights;
     for (int k = 0; k < s->n_lights; ++k) {
         for (int q = 0; q < 3; ++q) {
@@ -331,6 +376,73 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     for (int k = s->n_spheres; k < np; ++k) {                                   // padding: never a hit
         sph[k].r2 = -inf;
         sphf[k].rm = -std::numeric_limits<float>::infinity();
+    }
+    // Meshes (Tetrahedron :863-900, Cube :903-950): Shape(p, m, sqrt(3)*edge/2, false) with Triangle /
+    // Quad sub-objects at zero position.  World vertex 0 of a triangle: tetrahedron (zero + (p + bc)) + v0,
+    // cube (zero + (zero + (p + bc))) + v0 — the chain of `_position + positionOffset` additions (:739, :640).
+    rt::DevMesh* dmesh = reinterpret_cast<rt::DevMesh*>(reinterpret_cast<rt::DevSpherePrimF*>(sphf + np) + np);
+    rt::DevTri* dtri = reinterpret_cast<rt::DevTri*>(dmesh + s->n_meshes);
+    d->n_meshes = s->n_meshes;
+    d->n_tris = n_tris;
+    int t_next = 0;
+    for (int m = 0; m < s->n_meshes; ++m) {
+        const rt_mesh& M = s->meshes[m];
+        rt::DevMesh& DM = dmesh[m];
+        const HP mpos = hp(M.position) + bc;                                    // Shape: _position + offset
+        const double radius = std::sqrt((double)3) * M.edge / 2;
+        put(DM.bc, mpos);
+        DM.br2 = radius * radius;
+        DM.inner2 = radius > 2 ? (radius - 1) * (radius - 1) : -1.0;
+        DM.tri0 = t_next;
+        DM.child = (s->has_board ? 1 : 0) + M.after_spheres + m;
+        const double h = M.edge / 2;
+        std::vector<std::array<HP, 3>> tris;
+        HP tpos;
+        if (M.kind == RT_MESH_TETRAHEDRON) {
+            DM.mat = 3;
+            DM.per_face = 1;
+            DM.nfaces = 4;
+            tris = {{hp(-h, -h, -h), hp(h, -h, -h), hp(-h, -h, h)},                 // bottom
+                    {hp(-h, -h, -h), hp(-h, -h, h), hp(-h, h, -h)},                 // back
+                    {hp(-h, -h, -h), hp(-h, h, -h), hp(-h, -h, h)},                 // left
+                    {hp(-h, -h, h), hp(h, -h, -h), hp(-h, h, -h)}};                 // front
+            tpos = zero + mpos;
+        } else {
+            DM.mat = 4;
+            DM.per_face = 2;
+            DM.nfaces = 6;
+            const HP q[6][4] = {{hp(-h, h, -h), hp(h, h, -h), hp(h, h, h), hp(-h, h, h)},        // top
+                                {hp(-h, -h, -h), hp(h, -h, -h), hp(h, -h, h), hp(-h, -h, h)},    // bottom
+                                {hp(-h, -h, -h), hp(-h, h, -h), hp(-h, h, h), hp(-h, -h, h)},    // left
+                                {hp(h, -h, -h), hp(h, h, -h), hp(h, h, h), hp(h, -h, h)},        // right
+                                {hp(-h, -h, -h), hp(h, -h, -h), hp(h, h, -h), hp(-h, h, -h)},    // back
+                                {hp(-h, -h, h), hp(h, -h, h), hp(h, h, h), hp(-h, h, h)}};       // front
+            for (int f = 0; f < 6; ++f) {                                       // Quad: T(p1,p2,p3), T(p1,p3,p4)
+                tris.push_back({q[f][0], q[f][1], q[f][2]});
+                tris.push_back({q[f][0], q[f][2], q[f][3]});
+            }
+            tpos = zero + (zero + mpos);
+        }
+        for (const auto& tv : tris) {
+            rt::DevTri& T = dtri[t_next++];
+            HP u = tv[1] - tv[0], v = tv[2] - tv[0];                            // :413-414
+            HP n = cross(u, v);                                                 // :415
+            bool degenerate = length(n) < s->small_number;                      // :418
+            n = normalize(n);                                                   // :422
+            double uv = dot(u, v), uu = dot(u, u), vv = dot(v, v);             // :424-426
+            double den = uv * uv - uu * vv;                                     // :428
+            if (std::fabs(den) < s->small_number) degenerate = true;            // :430
+            put(T.v0, tpos + tv[0]);                                            // :640-641
+            put(T.u, u);
+            put(T.v, v);
+            put(T.n, n);
+            T.uv = uv;
+            T.uu = uu;
+            T.vv = vv;
+            T.den = den;
+            T.thr = (den < 0 && std::fabs(den) >= 1024.0) ? std::ldexp(std::fabs(den), -1070) : inf;
+            T.degenerate = degenerate ? 1.0 : 0.0;
+        }
     }
     return RT_OK;
 }

@@ -70,7 +70,7 @@ __device__ __forceinline__ unsigned char to_u8(double c) {
     return (unsigned char)(int)floor(v * 255.0 + 0.5);
 }
 
-template <int B, int LDS, int MINW>
+template <int B, int LDS, int MINW, bool TRANSP>
 __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
                                                              RenderParams P, float4* __restrict__ out32,
                                                              uchar4* __restrict__ out8,
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
         d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(i + P.bottom_x), right)),
                     scl(P.pitch * (double)(j + P.bottom_y), upp));
         d3 bdP = sub(ld3(V.S->bc), eye);           // bounding-sphere deltaP for p0 = camera
-        col = trace<B, true>(V, eye, sp, bdP, dot(bdP, bdP), &seg, &sh);
+        col = trace<B, true, TRANSP>(V, eye, sp, bdP, dot(bdP, bdP), &seg, &sh);
     }
 
     // Stage through LDS, then store whole tile rows.
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(kThreads) void rt_prepare_kernel(DevScene* __restri
     primf[k] = f;
 }
 
-template <int B>
+template <int B, bool TRANSP>
 __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene* __restrict__ S,
                                                                  const double* __restrict__ starts,
                                                                  const double* __restrict__ ends, int n,
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
     if (k >= n) return;
     uint32_t seg = 0, sh = 0;
     const SceneView V = view_of(S, S, S->n_padded, S->n_lights);
-    d3 c = trace<B, false>(V, ld3(starts + 3 * k), ld3(ends + 3 * k), mk(0.0, 0.0, 0.0), 0.0, &seg, &sh);
+    d3 c = trace<B, false, TRANSP>(V, ld3(starts + 3 * k), ld3(ends + 3 * k), mk(0.0, 0.0, 0.0), 0.0, &seg, &sh);
     if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
     if (rc) rc[k] = seg | (sh << 16);
 }
@@ -198,15 +198,19 @@ __global__ __launch_bounds__(kThreads) void rt_intersect_kernel(const DevScene* 
     set_dir(&r, d, divs(d, len(d)));
     set_origin_f32(S, &r);
     d3 p;
-    int kind = closest_hit(V, r, &p);
+    int kind = closest_hit<true>(V, r, &p);
     rt_hit h;
     h.hit = kind >= 0;
     h.material = -1;
-    for (int q = 0; q < 3; ++q) { h.point[q] = 0.0; h.normal[q] = 0.0; h.reflected_end[q] = 0.0; }
+    for (int q = 0; q < 3; ++q) {
+        h.point[q] = 0.0; h.normal[q] = 0.0; h.reflected_end[q] = 0.0; h.transmitted_end[q] = 0.0;
+    }
     if (kind >= 0) {
         d3 n, pe;
         int mat;
         surface(V, kind, p, r.u, &n, &mat, &pe);
+        d3 pt = transmitted_end(V, kind, mat, p, r.u, n);
+        h.transmitted_end[0] = pt.x; h.transmitted_end[1] = pt.y; h.transmitted_end[2] = pt.z;
         h.material = mat;
         h.point[0] = p.x; h.point[1] = p.y; h.point[2] = p.z;
         h.normal[0] = n.x; h.normal[1] = n.y; h.normal[2] = n.z;
@@ -232,17 +236,17 @@ __global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* 
 
 // ------------------------------------------------------------------------------------------------
 // Template dispatch.
-template <int LDS, int MINW>
+template <int LDS, int MINW, bool TRANSP>
 hipError_t launch_render_lds(int depth, dim3 grid, size_t lds, hipStream_t st, const DevScene* s,
                              const RenderParams& P, float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
 #define RT_CASE(b)                                                                                      \
     case b:                                                                                             \
         if (lds > 65536) {                                                                              \
-            hipError_t e_ = hipFuncSetAttribute((const void*)rt_render_kernel<b, LDS, MINW>,                  \
+            hipError_t e_ = hipFuncSetAttribute((const void*)rt_render_kernel<b, LDS, MINW, TRANSP>,                  \
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);  \
             if (e_ != hipSuccess) return e_;                                                            \
         }                                                                                               \
-        hipLaunchKernelGGL((rt_render_kernel<b, LDS, MINW>), grid, dim3(kThreads), lds, st, s, P, o32, o8,    \
+        hipLaunchKernelGGL((rt_render_kernel<b, LDS, MINW, TRANSP>), grid, dim3(kThreads), lds, st, s, P, o32, o8,    \
                            o64, orc);                                                                   \
         break;
     switch (depth) {
@@ -253,11 +257,13 @@ hipError_t launch_render_lds(int depth, dim3 grid, size_t lds, hipStream_t st, c
     return hipGetLastError();
 }
 
+template <bool TRANSP>
 hipError_t launch_trace_rays(int depth, dim3 grid, hipStream_t st, const DevScene* s, const double* a,
                              const double* b, int n, double* rgb, uint32_t* rc) {
 #define RT_CASE(k)                                                                                      \
     case k:                                                                                             \
-        hipLaunchKernelGGL((rt_trace_rays_kernel<k>), grid, dim3(kThreads), 0, st, s, a, b, n, rgb, rc);\
+        hipLaunchKernelGGL((rt_trace_rays_kernel<k, TRANSP>), grid, dim3(kThreads), 0, st, s, a, b, n, rgb,\
+                           rc);                                                                         \
         break;
     switch (depth) {
         RT_CASE(0) RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7)
@@ -281,6 +287,7 @@ struct rt_ctx {
     int n_padded = 0;
     int n_lights = 0;
     bool scene_set = false;
+    bool transparent = false;                  // some material is transparent: TRANSP kernel variants
     bool eye_valid = false;                    // the device *Prim arrays hold data for `eye`
     double eye[3] = {0, 0, 0};
     int min_waves = 5;                         // __launch_bounds__(256, 5) for depth <= 3 (measured faster
@@ -357,6 +364,7 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     c->lds_bytes = h->lds_bytes;
     c->n_padded = h->n_padded;
     c->n_lights = h->n_lights;
+    c->transparent = h->transparent != 0 || h->n_meshes > 0;   // FULL kernel variants
     c->eye_valid = false;
     c->scene_set = true;
     return RT_OK;
@@ -422,12 +430,15 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
         memcpy(c->eye, cam->eye, sizeof(c->eye));
         c->eye_valid = true;
     }
-    if (c->use_lds)
-        e = launch_render_lds<1, 1>(depth, grid, c->lds_bytes + stage, st, c->d_scene, P,
+    if (c->transparent)
+        e = launch_render_lds<0, 1, true>(depth, grid, stage, st, c->d_scene, P, reinterpret_cast<float4*>(rgba32f),
+                                          reinterpret_cast<uchar4*>(rgba8), rgb64f, raycount);
+    else if (c->use_lds)
+        e = launch_render_lds<1, 1, false>(depth, grid, c->lds_bytes + stage, st, c->d_scene, P,
                                  reinterpret_cast<float4*>(rgba32f), reinterpret_cast<uchar4*>(rgba8), rgb64f,
                                  raycount);
     else
-        e = (c->min_waves >= 5 && depth <= 3 ? launch_render_lds<0, 5> : launch_render_lds<0, 1>)(
+        e = (c->min_waves >= 5 && depth <= 3 ? launch_render_lds<0, 5, false> : launch_render_lds<0, 1, false>)(
                 depth, grid, stage, st, c->d_scene, P, reinterpret_cast<float4*>(rgba32f),
                                  reinterpret_cast<uchar4*>(rgba8), rgb64f, raycount);
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_kernel launch: ") + hipGetErrorString(e));
@@ -493,7 +504,8 @@ extern "C" int rt_trace_rays_dev(rt_ctx* c, const double* starts, const double* 
     if (n == 0) return RT_OK;
     RT_HIP(hipSetDevice(c->device));
     dim3 grid((unsigned)((n + kThreads - 1) / kThreads));
-    hipError_t e = launch_trace_rays(depth, grid, (hipStream_t)stream, c->d_scene, starts, ends, n, rgb64f, raycount);
+    hipError_t e = (c->transparent ? launch_trace_rays<true> : launch_trace_rays<false>)(
+        depth, grid, (hipStream_t)stream, c->d_scene, starts, ends, n, rgb64f, raycount);
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_trace_rays_kernel: ") + hipGetErrorString(e));
     return RT_OK;
 }

@@ -5,7 +5,9 @@
 //   DevSphere[np]       FP64 exact data                 ┐ copied into LDS once per workgroup
 //   DevSpherePrim[np]   primary-ray FP64 data (per eye)  ┘ (lds_bytes)
 //   DevSphereF[np]      FP32 filter image               ┐ read through the scalar cache (SGPR operands),
-//   DevSpherePrimF[np]  primary-ray FP32 filter (per eye)┘ 8 records per s_load batch
+//   DevSpherePrimF[np]  primary-ray FP32 filter (per eye)┘ one batch of kChunk records per s_load group
+//   DevMesh[nm]         tetrahedra / cubes: bounding sphere, triangle range, material, child index
+//   DevTri[nt]          their triangles (world vertex 0, u, v, n, uv, uu, vv, den)
 // np = n_spheres rounded up to kChunk; the padding spheres have r2 = -inf and filter terms = -inf, so
 // they are rejected by the filter and can never hit.  The two *Prim arrays depend on the camera eye and
 // are (re)written on the device by rt_prepare_kernel whenever rt_render_dev sees a new eye.
@@ -27,12 +29,27 @@ struct alignas(16) DevTri {            // Triangle after its ctor (:406-433), ve
     double u[3], v[3], n[3];
     double uv, uu, vv, den;
     double thr;                        // |den| * 2^-1070: A > thr  =>  A/den < 0 and nonzero
-    double pad;
+    double degenerate;                 // 1.0: this triangle never intersects (:633-637)
 };
 
-struct alignas(16) DevMat {            // the three colour terms rayTraceRay reads (:1224-1226)
+struct alignas(16) DevMat {            // the colour terms rayTraceRay reads (:1224-1226) and its continuation
     double amb[3], diff[3], spec[3];
-    double pad;
+    double w[3];                       // weight of the child colour: transparency (transmit) or 1 - T (reflect)
+    double refr;                       // refraction ratio (transmitted ray, :686-697)
+    int32_t transmit;                  // 1: transmitted ray (:1238-1242), 0: reflected ray (:1243-1247)
+    int32_t transparent;               // transparency != 0: a shadow blocker of this material lets light pass (:1221)
+};
+
+struct alignas(16) DevMesh {           // Tetrahedron / Cube Shape (:863-950)
+    double bc[3];                      // _position + positionOffset (:739)
+    double br2;                        // radius^2, radius = sqrt(3)*edge/2
+    double inner2;                     // (radius - 1)^2 or -1 (bound-cull shortcut, as for g_scene)
+    int32_t tri0;                      // first DevTri
+    int32_t nfaces;                    // faces: 1 triangle each (tetrahedron) or 2 = Quad, first hit (cube)
+    int32_t per_face;                  // 1 or 2
+    int32_t mat;                       // material index (3 tetrahedron, 4 cube)
+    int32_t child;                     // index in g_scene's child list (closest-hit tie order)
+    int32_t pad;
 };
 
 struct alignas(16) DevLight {
@@ -74,9 +91,12 @@ struct alignas(16) DevScene {
     int32_t n_padded;                  // np: n_spheres rounded up to kChunk
     int32_t n_lights;
     int32_t lds_bytes;                 // header + DevSphere[np] + DevSpherePrim[np]
-    int32_t pad0, pad1;
+    int32_t n_meshes;
+    int32_t n_tris;
+    int32_t transparent;               // some material is transparent: closest-hit shadows, weighted children
+    int32_t pad0;
     DevTri tri[2];                     // board triangles T1 = (P1,P2,P3), T2 = (P1,P3,P4)   (:840-841)
-    DevMat mat[3];                     // 0 white square, 1 black square, 2 sphere
+    DevMat mat[5];                     // 0 white square, 1 black square, 2 sphere, 3 tetrahedron, 4 cube
     DevLight light[16];
 };
 
@@ -86,8 +106,9 @@ inline constexpr int lds_bytes_for(int n) {
     return (int)(sizeof(DevScene) + (sizeof(DevSphere) + sizeof(DevSpherePrim)) * (unsigned)padded_spheres(n));
 }
 
-inline constexpr int scene_bytes_for(int n) {
-    return lds_bytes_for(n) + (int)((sizeof(DevSphereF) + sizeof(DevSpherePrimF)) * (unsigned)padded_spheres(n));
+inline constexpr int scene_bytes_for(int n, int n_meshes = 0, int n_tris = 0) {
+    return lds_bytes_for(n) + (int)((sizeof(DevSphereF) + sizeof(DevSpherePrimF)) * (unsigned)padded_spheres(n)) +
+           (int)(sizeof(DevMesh) * (unsigned)n_meshes + sizeof(DevTri) * (unsigned)n_tris);
 }
 
 }  // namespace rt

@@ -59,11 +59,22 @@ class LightSpec:
 
 
 @dataclass
+class MeshSpec:
+    """Tetrahedron(p, edge) / Cube(p, edge) at convertStringCoordinate(square) (MySdlApplication.cpp:863-950),
+    placed in g_scene's child list after `after_spheres` spheres."""
+    kind: int                      # abi.RT_MESH_TETRAHEDRON / abi.RT_MESH_CUBE
+    square: str
+    after_spheres: int = 0
+    edge: float = 40.0             # SQUARE_EDGE_SIZE, as loadScene/initScene use
+
+
+@dataclass
 class Scene:
-    """A g_scene: board (first child) + spheres, and the light list of one frame."""
+    """A g_scene: board (first child) + spheres and meshes, and the light list of one frame."""
     spheres: List[SphereSpec] = field(default_factory=list)
     lights: List[LightSpec] = field(default_factory=list)
     has_board: bool = True
+    meshes: List[MeshSpec] = field(default_factory=list)
     _keep: list = field(default_factory=list, repr=False)
 
     def to_abi(self) -> abi.rt_scene:
@@ -80,46 +91,85 @@ class Scene:
         for k, lt in enumerate(self.lights):
             lts[k].color = abi.vec3(lt.color)
             lts[k].position = abi.vec3(lt.position())
-        s.n_spheres, s.n_lights = ns, nl
+        nm = len(self.meshes)
+        msh = (abi.rt_mesh * max(nm, 1))()
+        for k, m in enumerate(self.meshes):
+            msh[k].kind = m.kind
+            msh[k].after_spheres = m.after_spheres
+            msh[k].position = abi.vec3(convert_string_coordinate(m.square))
+            msh[k].edge = float(m.edge)
+        s.n_spheres, s.n_lights, s.n_meshes = ns, nl, nm
         s.spheres = ctypes.cast(sph, ctypes.POINTER(abi.rt_sphere))
         s.lights = ctypes.cast(lts, ctypes.POINTER(abi.rt_light))
-        self._keep = [sph, lts]          # keep the arrays alive as long as the Scene
+        s.meshes = ctypes.cast(msh, ctypes.POINTER(abi.rt_mesh))
+        self._keep = [sph, lts, msh]     # keep the arrays alive as long as the Scene
         return s
+
+    def children(self) -> List[Tuple[str, int]]:
+        """g_scene child order after the board: ('S', k) spheres and ('M', m) meshes."""
+        out, m = [], 0
+        for k in range(len(self.spheres) + 1):
+            while m < len(self.meshes) and self.meshes[m].after_spheres <= k:
+                out.append(("M", m))
+                m += 1
+            if k < len(self.spheres):
+                out.append(("S", k))
+        out.extend(("M", i) for i in range(m, len(self.meshes)))
+        return out
 
     # the reference harness (oracle/_ref) rebuilds the same scene from the reference's own classes
     def ref_args(self):
-        ns, nl = len(self.spheres), len(self.lights)
-        sq = "".join(sp.square for sp in self.spheres).encode()
+        if not self.has_board:
+            raise ValueError("the reference harness always inserts the board")
+        ns, nl, nm = len(self.spheres), len(self.lights), len(self.meshes)
+        toks = []
+        for kind, i in self.children():
+            if kind == "S":
+                toks.append("S" + self.spheres[i].square)
+            else:
+                m = self.meshes[i]
+                toks.append(("T" if m.kind == abi.RT_MESH_TETRAHEDRON else "C") + m.square)
+        children = "".join(toks).encode()
         yoff = (ctypes.c_double * max(ns, 1))(*[sp.y_offset for sp in self.spheres])
         rad = (ctypes.c_double * max(ns, 1))(*[sp.radius for sp in self.spheres])
+        edges = (ctypes.c_double * max(nm, 1))(*[m.edge for m in self.meshes])
         if any(lt.square is None for lt in self.lights):
             raise ValueError("the reference harness places lights by square")
         lsq = "".join(lt.square for lt in self.lights).encode()
         lcol = (ctypes.c_double * max(3 * nl, 1))(*[c for lt in self.lights for c in lt.color])
-        return (sq, yoff, rad, ns, lsq, lcol, nl)
+        return (children, len(toks), yoff, rad, edges, lsq, lcol, nl)
 
 
 def load_scene(entries: Sequence[Tuple[str, int]]) -> Scene:
     """loadScene semantics (MySdlApplication.cpp:1495-1539) via the C ABI: later duplicates win, entries
-    are visited in std::map<string> order, the last light wins, one white light.  Mesh types raise
-    RtError(RT_EUNSUPPORTED)."""
+    are visited in std::map<string> order, the last light wins, one white light.  Cylinders / cones raise
+    RtError(RT_EUNSUPPORTED) (reference stubs)."""
     L = abi.lib()
     n = len(entries)
     squares = (ctypes.c_char_p * max(n, 1))(*[e[0].encode() for e in entries])
     types = (ctypes.c_int32 * max(n, 1))(*[int(e[1]) for e in entries])
     s = abi.rt_scene()
     buf = (abi.rt_sphere * max(n, 1))()
+    mbuf = (abi.rt_mesh * max(n, 1))()
     light = abi.rt_light()
-    abi.check(L.rt_load_scene(squares, types, n, ctypes.byref(s), buf, max(n, 1), ctypes.byref(light)),
-              "rt_load_scene")
+    abi.check(L.rt_load_scene(squares, types, n, ctypes.byref(s), buf, max(n, 1), mbuf, max(n, 1),
+                              ctypes.byref(light)), "rt_load_scene")
     board = {}
     for sq, t in entries:
         board[sq] = t
-    spheres = [SphereSpec(sq, 20.0) for sq in sorted(board) if board[sq] == SPHERE]
-    lights_sq = [sq for sq in sorted(board) if board[sq] == LIGHT]
+    spheres, meshes, lights_sq = [], [], []
+    for sq in sorted(board):                 # std::map<string> order = byte order of the 2-char keys
+        t = board[sq]
+        if t == SPHERE:
+            spheres.append(SphereSpec(sq, 20.0))
+        elif t in (TETRAHEDRON, CUBE):
+            meshes.append(MeshSpec(abi.RT_MESH_TETRAHEDRON if t == TETRAHEDRON else abi.RT_MESH_CUBE, sq,
+                                   after_spheres=len(spheres)))
+        elif t == LIGHT:
+            lights_sq.append(sq)
     # draw() always pushes one light; with no light entry g_lightPosition keeps its default (0,0,0)
-    scene = Scene(spheres=spheres, lights=[LightSpec(lights_sq[-1] if lights_sq else None)])
-    scene._abi_loaded = (s, buf, light)
+    scene = Scene(spheres=spheres, lights=[LightSpec(lights_sq[-1] if lights_sq else None)], meshes=meshes)
+    scene._abi_loaded = (s, buf, mbuf, light)
     return scene
 
 
@@ -138,6 +188,10 @@ class Config:
         return 500.0 / self.width          # canonical framing
 
     def scene(self) -> Scene:
+        if self.name == "demo":
+            # initScene (MySdlApplication.cpp:1387-1428): board, tetrahedron b4, sphere d7 (r 20), cube a7
+            return Scene(spheres=[SphereSpec("d7", 20.0)], lights=[LightSpec("b6", WHITE)],
+                         meshes=[MeshSpec(abi.RT_MESH_TETRAHEDRON, "b4", 0), MeshSpec(abi.RT_MESH_CUBE, "a7", 1)])
         if self.n_spheres == 64:
             sph = [SphereSpec(chr(ord("a") + r) + chr(ord("1") + c), 10.0, float(((r + c) % 3) * 25))
                    for r in range(8) for c in range(8)]
@@ -167,10 +221,15 @@ CONFIGS = {
     "c3": Config("c3", 3840, 2160, 8, 2, 2),
     "c4": Config("c4", 3840, 2160, 8, 2, 2, gpus=8),
     "c5": Config("c5", 7680, 4320, 64, 2, 3, gpus=8),
+    # the reference app's own demo frame: initScene's objects, 500x500 window, unit pitch, MAX_DEPTH 5
+    "demo": Config("demo", 500, 500, 1, 1, 5),
 }
 
 # Pinned actual-traced ray counts (from the reference's rayTraceRay)
-PINNED_RAYS = {"c1": 380_817, "c2": 3_684_271, "c3": 18_956_255, "c5": 90_722_787}
+PINNED_RAYS = {"c1": 380_817, "c2": 3_684_271, "c3": 18_956_255, "c5": 90_722_787,
+               # the demo frame is not in SURVEY.md; pinned by the restatement, which matches the reference
+               # build bit for bit on this frame (tests/test_oracle.py)
+               "demo": 358_434}
 
 
 def rows(band_height: int = 1, n_ranks: int = 1, rank: int = 0) -> abi.rt_rows:

@@ -120,7 +120,7 @@ def decode_hits(raw: torch.Tensor) -> dict:
     import numpy as np
     a = raw.cpu().numpy()
     n = a.shape[0]
-    d = a[:, :72].copy().view(np.float64).reshape(n, 9)
-    i = a[:, 72:80].copy().view(np.int32).reshape(n, 2)
-    return {"point": d[:, 0:3], "normal": d[:, 3:6], "reflected_end": d[:, 6:9], "hit": i[:, 0],
-            "material": i[:, 1]}
+    d = a[:, :96].copy().view(np.float64).reshape(n, 12)
+    i = a[:, 96:104].copy().view(np.int32).reshape(n, 2)
+    return {"point": d[:, 0:3], "normal": d[:, 3:6], "reflected_end": d[:, 6:9], "transmitted_end": d[:, 9:12],
+            "hit": i[:, 0], "material": i[:, 1]}

@@ -10,7 +10,7 @@ Outputs (all small, committed):
   frames_<cfg>.npz   160x120 full frame (float64 RGB, pitch 500/160) + 4096 sampled pixels of the
                      full-resolution frame (i, j, float64 RGB)
   kat_<scene>.npz    primitive known-answer tests: rays -> Shape::intersection (hit, material, point,
-                     normal, reflected end) and rayTraceRay colours at depth 0..3
+                     normal, reflected and transmitted ends) and rayTraceRay colours at depth 0..5
   manifest.json      FNV-1a 64 of every full-resolution float64 frame, image sizes, provenance
 
 Run in the build container (needs /root/reference):  python tests/golden/make_golden.py
@@ -33,7 +33,7 @@ from ray_tracer_fragment_shader_amd import scenes  # noqa: E402
 OUT = os.path.dirname(os.path.abspath(__file__))
 SMALL_W, SMALL_H = 160, 120
 N_SAMPLES = 4096
-CFGS = ["c1", "c2", "c3", "c5"]
+CFGS = ["c1", "c2", "c3", "c5", "demo"]
 
 
 def sample_pixels(cfg, rng):
@@ -58,6 +58,24 @@ def kat_rays(scene, rng):
 
     centres = [np.array(sp.center()) + np.array([0.0, 0.0, -160.0]) for sp in scene.spheres]
     radii = [sp.radius for sp in scene.spheres]
+    # meshes: centre, vertices, edge midpoints, face interiors, from inside, grazing the bounding sphere
+    from ray_tracer_fragment_shader_amd.scenes import convert_string_coordinate
+    for m in scene.meshes:
+        c = np.array(convert_string_coordinate(m.square)) + np.array([0.0, 0.0, -160.0])
+        h = m.edge / 2
+        add(cam, c, "mesh_centre")
+        add(c, c + np.array([0.3, 1.0, -0.2]), "inside_mesh")
+        add(c, c + np.array([-1.0, -0.1, 0.05]), "inside_mesh")
+        for sx in (-1, 1):
+            for sy in (-1, 1):
+                for sz in (-1, 1):
+                    add(cam, c + h * np.array([sx, sy, sz]), "mesh_vertex")
+                    add(cam, c + 0.999 * h * np.array([sx, sy, sz]), "mesh_near_vertex")
+        for k in range(24):
+            add(cam, c + rng.uniform(-h, h, 3), "mesh_interior")
+        rb = np.sqrt(3.0) * m.edge / 2
+        add(cam, c + np.array([rb, 0, 0]) * (1 - 1e-9), "mesh_bound_graze")
+        add(c + np.array([0.0, 3 * h, 0.0]), c + np.array([0.0, -3 * h, 0.0]), "mesh_vertical")
     for c, r in zip(centres, radii):
         add(cam, c, "sphere_centre")
         add(c, c + np.array([1.0, 0.3, 0.2]), "inside_sphere")
@@ -127,15 +145,16 @@ def main() -> None:
                                     "nonzero_pixels": int((full.sum(axis=2) > 0).sum())}
         del full
         print(f"{name}: frames in {time.time() - t0:.1f}s hash {h:016x}", flush=True)
-    for name in ("c3", "c5"):
+    for name in ("c3", "c5", "demo"):
         cfg = scenes.CONFIGS[name]
         sc = cfg.scene()
         starts, ends, tags = kat_rays(sc, rng)
         inter = po.ref_intersect(sc, starts, ends)
-        colors = np.stack([po.ref_trace_rays(sc, starts, ends, d) for d in range(4)])
+        colors = np.stack([po.ref_trace_rays(sc, starts, ends, d) for d in range(6)])
         np.savez_compressed(os.path.join(OUT, f"kat_{name}.npz"), starts=starts, ends=ends, tags=tags,
                             hit=inter["hit"], material=inter["material"], point=inter["point"],
-                            normal=inter["normal"], reflected_end=inter["reflected_end"], colors=colors)
+                            normal=inter["normal"], reflected_end=inter["reflected_end"],
+                            transmitted_end=inter["transmitted_end"], colors=colors)
         print(f"kat_{name}: {len(starts)} rays, {int(inter['hit'].sum())} hits", flush=True)
     with open(os.path.join(OUT, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

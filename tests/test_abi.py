@@ -35,8 +35,9 @@ def test_struct_layouts_match_header_sizes():
     assert ctypes.sizeof(abi.rt_light) == 48
     assert ctypes.sizeof(abi.rt_camera) == 10 * 8 + 8
     assert ctypes.sizeof(abi.rt_rows) == 16
-    assert ctypes.sizeof(abi.rt_hit) == 80
-    assert ctypes.sizeof(abi.rt_scene) == 4 * 8 + 16 + 3 * 8 + 4 * 8 + 3 * 13 * 8 + 16
+    assert ctypes.sizeof(abi.rt_hit) == 104
+    assert ctypes.sizeof(abi.rt_mesh) == 40
+    assert ctypes.sizeof(abi.rt_scene) == 4 * 8 + 16 + 3 * 8 + 4 * 8 + 3 * 13 * 8 + 16 + 2 * 13 * 8 + 8 + 8
 
 
 def test_no_device_fails_loudly():
@@ -58,6 +59,8 @@ def test_reference_constants_and_materials():
     assert list(s.white_square.ambient) == [0.1] * 3 and list(s.white_square.diffuse) == [0.5] * 3
     assert list(s.black_square.diffuse) == [0.1] * 3 and list(s.black_square.specular) == [0.0] * 3
     assert list(s.sphere_material.specular) == [1.0] * 3 and list(s.sphere_material.ambient) == [0.0] * 3
+    assert list(s.tetrahedron_material.transparency) == [1.0] * 3 and s.tetrahedron_material.refraction == 2.0 / 3.0
+    assert list(s.cube_material.ambient) == [0.1, 0.0, 0.0] and list(s.cube_material.diffuse) == [0.4, 0.0, 0.0]
 
 
 def test_convert_string_coordinate():
@@ -84,7 +87,7 @@ def test_load_scene_semantics():
     S, L = scenes.SPHERE, scenes.LIGHT
     entries = [("d7", S), ("b6", L), ("a1", S), ("d7", S), ("c3", L), ("b2", S), ("b2", L)]
     sc = scenes.load_scene(entries)
-    s, buf, light = sc._abi_loaded
+    s, buf, mbuf, light = sc._abi_loaded
     # map order: a1, b2, b6, c3, d7 ; b2 was overwritten by LIGHT -> spheres a1, d7 ; last light c3
     assert s.n_spheres == 2
     assert [tuple(buf[k].center) for k in range(2)] == [scenes.convert_string_coordinate("a1"),
@@ -94,8 +97,24 @@ def test_load_scene_semantics():
     assert s.n_lights == 1 and list(light.color) == [1.0, 1.0, 1.0]
     assert [sp.square for sp in sc.spheres] == ["a1", "d7"]
     with pytest.raises(abi.RtError) as e:
-        scenes.load_scene([("a1", scenes.CUBE)])
+        scenes.load_scene([("a1", scenes.CYLINDER)])
     assert e.value.code == abi.RT_EUNSUPPORTED
+    with pytest.raises(abi.RtError) as e:
+        scenes.load_scene([("a1", scenes.CONE)])
+    assert e.value.code == abi.RT_EUNSUPPORTED
+
+
+def test_load_scene_meshes_child_order():
+    T, C, S, L = scenes.TETRAHEDRON, scenes.CUBE, scenes.SPHERE, scenes.LIGHT
+    sc = scenes.load_scene([("b4", T), ("d7", S), ("a7", C), ("b6", L), ("c2", S), ("h1", C)])
+    s, buf, mbuf, light = sc._abi_loaded
+    # map order: a7 (cube), b4 (tetra), b6 (light), c2 (sphere), d7 (sphere), h1 (cube)
+    assert s.n_meshes == 3 and s.n_spheres == 2
+    assert [(mbuf[k].kind, mbuf[k].after_spheres) for k in range(3)] == [(abi.RT_MESH_CUBE, 0),
+                                                                       (abi.RT_MESH_TETRAHEDRON, 0),
+                                                                       (abi.RT_MESH_CUBE, 2)]
+    assert tuple(mbuf[0].position) == scenes.convert_string_coordinate("a7") and mbuf[0].edge == 40.0
+    assert [k for k, _ in sc.children()] == ["M", "M", "S", "S", "M"]
 
 
 def test_camera_reference():

@@ -42,12 +42,16 @@ def _render64(tr, scene, cam, W, H, depth, rows=None):
 
 
 def _assert_parity(got, want):
-    err = np.abs(got - want).max() if got.size else 0.0
+    # NaN appears only where the reference itself yields NaN (total internal reflection -> Line(p, p))
+    assert np.array_equal(np.isnan(got), np.isnan(want)), "NaN pattern differs"
+    fin = ~np.isnan(want)
+    err = np.abs(got[fin] - want[fin]).max() if fin.any() else 0.0
     assert err <= TOL, f"L-inf {err}"
-    assert np.array_equal(got, want), f"not bit-exact: {(got != want).any(axis=-1).sum()} pixels differ"
+    assert np.array_equal(got, want, equal_nan=True), \
+        f"not bit-exact: {(got != want).any(axis=-1).sum()} pixels differ"
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c5"])
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c5", "demo"])
 def test_small_frame_vs_reference(tr, name):
     cfg = scenes.CONFIGS[name]
     g = golden.frames(name)
@@ -56,7 +60,7 @@ def test_small_frame_vs_reference(tr, name):
     _assert_parity(rgb, g["small"])
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c5"])
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c5", "demo"])
 def test_sampled_full_res_pixels_vs_reference(tr, name):
     cfg = scenes.CONFIGS[name]
     g = golden.frames(name)
@@ -68,7 +72,7 @@ def test_sampled_full_res_pixels_vs_reference(tr, name):
     _assert_parity(rgb.cpu().numpy(), g["samples"])
 
 
-@pytest.mark.parametrize("name", ["c1", "c2"])
+@pytest.mark.parametrize("name", ["c1", "c2", "demo"])
 def test_full_frame_vs_oracle(tr, name):
     cfg = scenes.CONFIGS[name]
     sc = cfg.scene()
@@ -89,7 +93,7 @@ def test_full_frame_hash_vs_reference(tr, name):
     assert int((rc & 0xFFFF).sum()) + int((rc >> 16).sum()) == scenes.PINNED_RAYS[name]
 
 
-@pytest.mark.parametrize("name", ["c3", "c5"])
+@pytest.mark.parametrize("name", ["c3", "c5", "demo"])
 def test_intersection_kat(tr, name):
     cfg = scenes.CONFIGS[name]
     k = golden.kat(name)
@@ -98,18 +102,18 @@ def test_intersection_kat(tr, name):
     got = decode_hits(raw)
     assert np.array_equal(got["hit"], k["hit"])
     assert np.array_equal(got["material"], k["material"])
-    for f in ("point", "normal", "reflected_end"):
+    for f in ("point", "normal", "reflected_end", "transmitted_end"):
         assert np.array_equal(got[f], k[f]), f
 
 
-@pytest.mark.parametrize("name", ["c3", "c5"])
+@pytest.mark.parametrize("name", ["c3", "c5", "demo"])
 def test_trace_rays_kat(tr, name):
     cfg = scenes.CONFIGS[name]
     k = golden.kat(name)
     tr.set_scene(cfg.scene())
     s = torch.tensor(k["starts"], device="cuda")
     e = torch.tensor(k["ends"], device="cuda")
-    for depth in range(4):
+    for depth in range(6):
         rgb, _ = tr.trace_rays(s, e, depth)
         _assert_parity(rgb.cpu().numpy(), k["colors"][depth])
 
@@ -217,7 +221,7 @@ def test_errors_are_loud(tr):
     cfg = scenes.CONFIGS["c1"]
     sc = cfg.scene()
     s = sc.to_abi()
-    s.sphere_material.transparency[0] = 1.0
+    s.sphere_material.transparency[0] = 0.5          # transmit AND reflect: a ray tree
     assert L.rt_set_scene(tr._ctx, ctypes.byref(s)) == abi.RT_EUNSUPPORTED
     s = sc.to_abi()
     s.n_spheres = abi.RT_MAX_SPHERES + 1
@@ -279,4 +283,49 @@ def test_cli_initscene2_dialogue_ppm(tmp_path):
     sc = scenes.load_scene([("d7", scenes.SPHERE), ("b2", scenes.SPHERE), ("b6", scenes.LIGHT)])
     cam = scenes.make_camera(500, 500, 1.0)
     want, _ = po.render(sc.to_abi(), cam, 500, 500, 5)
+    assert np.array_equal(_read_ppm(out), _ppm_expect(want))
+
+
+def _random_mesh_scene(rng):
+    entries = []
+    for _ in range(int(rng.integers(1, 14))):
+        sq = chr(ord("a") + int(rng.integers(0, 8))) + chr(ord("1") + int(rng.integers(0, 8)))
+        entries.append((sq, int(rng.choice([scenes.SPHERE, scenes.TETRAHEDRON, scenes.CUBE]))))
+    entries.append((chr(ord("a") + int(rng.integers(0, 8))) + chr(ord("1") + int(rng.integers(0, 8))), scenes.LIGHT))
+    return scenes.load_scene(entries)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_mesh_scenes_vs_oracle(tr, seed):
+    """loadScene boards with tetrahedra (transparent, refracting), cubes and spheres: frames and random rays."""
+    rng = np.random.default_rng(1000 + seed)
+    sc = _random_mesh_scene(rng)
+    W, H = 128, 96
+    cam = scenes.make_camera(W, H, float(rng.uniform(0.8, 4.0)))
+    depth = int(rng.integers(0, 8))
+    rgb, rc = _render64(tr, sc, cam, W, H, depth)
+    want, want_rc = po.render(sc.to_abi(), cam, W, H, depth)
+    _assert_parity(rgb, want)
+    assert np.array_equal(rc, want_rc)
+    s = rng.uniform(-250, 250, (2048, 3))
+    e = s + rng.normal(size=(2048, 3)) * rng.uniform(0.1, 100, (2048, 1))
+    g, _ = tr.trace_rays(torch.tensor(s, device="cuda"), torch.tensor(e, device="cuda"), depth)
+    w, _ = po.trace_rays(sc.to_abi(), s, e, depth)
+    _assert_parity(g.cpu().numpy(), w)
+    raw = tr.intersect(torch.tensor(s, device="cuda"), torch.tensor(e, device="cuda"))
+    got = decode_hits(raw)
+    want_h = po.intersect(sc.to_abi(), s, e)
+    for f in ("hit", "material", "point", "normal", "reflected_end", "transmitted_end"):
+        assert np.array_equal(got[f], want_h[f], equal_nan=True), f
+
+
+def test_cli_demo_ppm(tmp_path):
+    import subprocess
+    exe = os.path.join(os.path.dirname(abi.LIB_PATH), "rt_render")
+    out = tmp_path / "demo.ppm"
+    r = subprocess.run([exe, "--config", "demo", "--out", str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert f"rays {scenes.PINNED_RAYS['demo']}" in r.stdout
+    cfg = scenes.CONFIGS["demo"]
+    want, _ = po.render(cfg.scene().to_abi(), cfg.camera(), cfg.width, cfg.height, cfg.depth)
     assert np.array_equal(_read_ppm(out), _ppm_expect(want))
