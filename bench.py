@@ -8,11 +8,13 @@ parity image) and the RGBA8 display image, all buffers resident in HBM.  Rays ar
 actually-traced count (primary + reflected + shadow), taken from the kernel's own
 per-pixel ray counters before the timed region and checked against the reference's pinned total.
 
-N>1 (torch.distributed.run, one rank per GPU, RCCL): weak scaling by default — a step is N frames, every
-frame row-banded over all N ranks (band height 8, round-robin), each rank's slabs of all N frames
-gathered to rank 0 over RCCL in one collective, and rank 0 puts every frame back into image order with
-rt_unshuffle_dev.  Per-GPU work stays one frame.  `--scaling strong` renders ONE frame per step split
-over the N ranks (the c4 design).
+N>1 (torch.distributed.run, one rank per GPU, RCCL): weak scaling by default ("frame streams") — a step
+is N frames, one per rank as its display; every frame is row-banded over all N ranks (round-robin bands, height
+chosen so every rank gets the same rows), each rank renders its bands of all N frames in ONE launch (rt_rows.frames = N), one RCCL
+all-to-all sends frame f's rows to rank f, and rank f puts them in image order with rt_unshuffle_dev.
+Per-GPU work stays one frame; the exchange and the assembly of step s overlap the render of step s+1
+(double-buffered RGBA8 slabs, a side stream).  `--scaling strong` renders ONE frame per step split over
+the N ranks and gathers it to rank 0 (the c4 design).
 
 Printed: ONE JSON line on rank 0 (contract in the task statement) with `roofline` (HBM-write roofline of
 the dominant kernel, per north_star) and `roofline_fp64` (its FP64 VALU roofline) and `cpu_baseline`
@@ -44,7 +46,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c5"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
-    ap.add_argument("--band-height", type=int, default=8)
+    ap.add_argument("--band-height", type=int, default=0, help="0: auto (equal rows per rank)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--profile-kernel-only", action="store_true",
@@ -84,7 +86,8 @@ def main() -> int:
     import torch.distributed as dist
 
     from ray_tracer_fragment_shader_amd import scenes
-    from ray_tracer_fragment_shader_amd.distributed import BandPlan, assemble_on_device, gather_slabs
+    from ray_tracer_fragment_shader_amd.distributed import (BandPlan, assemble_on_device, exchange_frames,
+                                                            gather_slabs)
     from ray_tracer_fragment_shader_amd.tracer import Tracer
 
     if not torch.cuda.is_available():
@@ -107,14 +110,24 @@ def main() -> int:
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream(dev)
 
-    frames = world if (world > 1 and args.scaling == "weak") else 1
-    plan = BandPlan(H, world, args.band_height)
+    weak = world > 1 and args.scaling == "weak"
+    frames = world if weak else 1
+    plan = BandPlan(H, world, args.band_height, frames=frames)
+    if weak and not plan.balanced:
+        raise SystemExit(f"frame streams need equal rows per rank: H={H}, N={world}, band {plan.band_height}")
     rows = plan.rows(rank) if world > 1 else None
-    nl = plan.local[rank]
-    slab = plan.slab_rows
-    out32 = torch.empty((frames, slab, W, 4), dtype=torch.float32, device=dev)
-    out8 = torch.empty((frames, slab, W, 4), dtype=torch.uint8, device=dev)
-    image8 = torch.empty((frames, H, W, 4), dtype=torch.uint8, device=dev) if (rank == 0 and world > 1) else None
+    nl = plan.local[rank]                  # rows this rank renders per step (all its frames)
+    fl = plan.frame_local[rank]            # ... per frame
+    out32 = torch.empty((nl, W, 4), dtype=torch.float32, device=dev)
+    out8 = [torch.empty((nl, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
+    if weak:
+        recv8 = [torch.empty((world, fl, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
+        image8 = [torch.empty((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
+        side = torch.cuda.Stream(dev)
+        assembled = [torch.cuda.Event() for _ in range(2)]
+        pending = [None, None]
+    elif world > 1 and rank == 0:
+        image8 = [torch.empty((H, W, 4), dtype=torch.uint8, device=dev)]
 
     # ---- parity + ray count (outside the timed region) ----------------------------------------------
     parity = "skipped"
@@ -140,21 +153,30 @@ def main() -> int:
     from ray_tracer_fragment_shader_amd import abi
     fn = abi.lib().rt_render_dev
     rows_ref = ctypes.byref(rows) if rows is not None else None
-    launch_args = [(tr._ctx, ctypes.byref(cam), W, H, B, rows_ref, ctypes.c_void_p(out32[f].data_ptr()),
-                    ctypes.c_void_p(out8[f].data_ptr()), None, None, ctypes.c_void_p(stream.cuda_stream))
-                   for f in range(frames)]
+    launch_args = [(tr._ctx, ctypes.byref(cam), W, H, B, rows_ref, ctypes.c_void_p(out32.data_ptr()),
+                    ctypes.c_void_p(out8[b].data_ptr()), None, None, ctypes.c_void_p(stream.cuda_stream))
+                   for b in range(2)]
+    counter = [0]
 
     def step():
-        for f in range(frames):
-            rc = fn(*launch_args[f])
-            if rc:
-                abi.check(rc, "rt_render_dev")
-        if world > 1:
-            gathered = gather_slabs(out8, world)
+        b = counter[0] % 2
+        counter[0] += 1
+        if weak and pending[b] is not None:
+            pending[b].wait()                               # the all-to-all of step s-2 has read out8[b]
+        rc = fn(*launch_args[b])
+        if rc:
+            abi.check(rc, "rt_render_dev")
+        if weak:
+            stream.wait_event(assembled[b])                 # recv8[b] consumed by the assembly of step s-2
+            pending[b] = exchange_frames(out8[b].view(world, fl, W, 4), recv8[b], world, async_op=True)
+            with torch.cuda.stream(side):
+                pending[b].wait()
+                assemble_on_device(recv8[b], plan, W, image8[b], side)
+                assembled[b].record(side)
+        elif world > 1:
+            gathered = gather_slabs(out8[b], world)
             if rank == 0:
-                allr = torch.stack(gathered)                 # [world, frames, slab, W, 4]
-                for f in range(frames):
-                    assemble_on_device(allr[:, f].contiguous(), plan, W, image8[f], stream)
+                assemble_on_device(torch.stack(gathered), plan, W, image8[0], stream)
 
     for _ in range(args.warmup):
         step()
@@ -167,13 +189,13 @@ def main() -> int:
     for _ in range(args.steps):
         step()
     ev1.record(stream)
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()                                # every stream: render, exchange, assembly
     barrier()
     elapsed = time.perf_counter() - t0
     if world == 1:
         # HIP events on the launch stream bracketing the timed region, which holds only the K launches of
         # rt_render_kernel (per-launch event pairs would serialise the queue and add ~8 us per launch).
-        avg_kern_ms = ev0.elapsed_time(ev1) / (args.steps * frames)
+        avg_kern_ms = ev0.elapsed_time(ev1) / args.steps
     else:
         # the timed region also holds the gather: time the kernel alone in a short post-pass
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -181,11 +203,10 @@ def main() -> int:
         torch.cuda.synchronize()
         e[0].record(stream)
         for _ in range(n):
-            for f in range(frames):
-                fn(*launch_args[f])
+            fn(*launch_args[0])
         e[1].record(stream)
         torch.cuda.synchronize()
-        avg_kern_ms = e[0].elapsed_time(e[1]) / (n * frames)
+        avg_kern_ms = e[0].elapsed_time(e[1]) / n
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -224,7 +245,10 @@ def main() -> int:
                             f"{B} bounce(s), pitch 500/W; step = {frames} frame(s)",
                 "width": W, "height": H, "spheres": cfg.n_spheres, "lights": cfg.n_lights, "bounces": B,
                 "rays_per_frame": rays_frame, "frames_per_step": frames,
-                "parallelism": f"row-bands(h={args.band_height}) x {world} + RCCL gather" if world > 1 else "single GPU",
+                "parallelism": (f"frame streams: {world} frames/step, row bands (h={plan.band_height}) x {world} "
+                                f"ranks, RCCL all-to-all" if weak else
+                                f"row bands (h={plan.band_height}) x {world} ranks + RCCL gather to rank 0"
+                                if world > 1 else "single GPU"),
             },
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

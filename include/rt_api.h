@@ -124,12 +124,14 @@ typedef struct rt_camera {
 
 /* Row banding for multi-GPU sharding: the image's rows are cut into bands of `band_height` rows and
  * band b goes to rank b % n_ranks.  A call renders only its rank's rows, densely, in increasing order.
- * NULL rt_rows* (or n_ranks == 1) means the full image. */
+ * `frames` > 1 renders that many frames of the same view in one call, frame-major: the rank's rows of
+ * frame 0, then of frame 1, ... (each frame banded the same way), so an all-to-all can send frame f's
+ * rows to rank f.  NULL rt_rows* (or n_ranks == 1 and frames <= 1) means one full image. */
 typedef struct rt_rows {
     int32_t band_height;
     int32_t n_ranks;
     int32_t rank;
-    int32_t reserved0;
+    int32_t frames;              /* 0 or 1: one frame */
 } rt_rows;
 
 /* Ray counts actually traced (SURVEY.md §8d rule): primary segments, reflected segments (levels 1..B,
@@ -180,9 +182,9 @@ int rt_load_scene(const char* const* squares, const int32_t* types, int n, rt_sc
                   rt_sphere* sphere_buf, int sphere_cap, rt_mesh* mesh_buf, int mesh_cap, rt_light* light);
 /* draw()'s camera (MySdlApplication.cpp:1556-1560) for a W x H window at the given pitch. */
 int rt_camera_init_reference(rt_camera* cam, int width, int height, double pitch);
-/* Number of image rows a rank renders under `rows` (NULL = all rows). */
+/* Number of rows a rank renders under `rows` (NULL = all rows), over all its frames. */
 int rt_local_rows(int height, const rt_rows* rows, int* out);
-/* Global image row of local row `local_row` under `rows`. */
+/* Image row of local row `local_row` under `rows`: frame * height + row within the frame. */
 int rt_global_row(int height, const rt_rows* rows, int local_row, int* out);
 
 /* ---- device path ---------------------------------------------------------------------------- */

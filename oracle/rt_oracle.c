@@ -461,14 +461,21 @@ static P screen_point(const rt_camera* c, P right, P upp, int i, int j) {
                scl(c->pitch * (double)(j + c->bottom_y), upp));
 }
 
-static int local_rows(int H, const rt_rows* r) {
+/* Row banding (rt_api.h rt_rows): rows of one frame owned by the rank, frames stacked frame-major. */
+static int frame_rows(int H, const rt_rows* r) {
     if (!r || r->n_ranks <= 1) return H;
     int hb = r->band_height, G = r->n_ranks, n = 0;
     for (int j = 0; j < H; ++j) if ((j / hb) % G == r->rank) ++n;
     return n;
 }
 
-static int global_row(const rt_rows* r, int lr) {
+static int local_rows(int H, const rt_rows* r) {
+    return frame_rows(H, r) * ((r && r->frames > 1) ? r->frames : 1);
+}
+
+/* row within its frame of local row lr */
+static int global_row(int H, const rt_rows* r, int lr) {
+    lr %= frame_rows(H, r);
     if (!r || r->n_ranks <= 1) return lr;
     int hb = r->band_height, G = r->n_ranks;
     int band = lr / hb, within = lr % hb;
@@ -494,7 +501,7 @@ int oracle_render(const rt_scene* d, const rt_camera* c, int W, int H, int depth
 #pragma omp parallel for schedule(dynamic, 1)
 #endif
     for (int lr = 0; lr < nl; ++lr) {
-        int j = global_row(rows, lr);
+        int j = global_row(H, rows, lr);
         for (int i = 0; i < W; ++i) {
             Line ray; ray.s = cam; ray.e = screen_point(c, right, upp, i, j);
             P col = pt(0.0, 0.0, 0.0);

@@ -77,7 +77,7 @@ class rt_camera(Structure):
 
 
 class rt_rows(Structure):
-    _fields_ = [("band_height", c_int32), ("n_ranks", c_int32), ("rank", c_int32), ("reserved0", c_int32)]
+    _fields_ = [("band_height", c_int32), ("n_ranks", c_int32), ("rank", c_int32), ("frames", c_int32)]
 
 
 class rt_stats(Structure):

@@ -183,22 +183,30 @@ extern "C" int rt_camera_init_reference(rt_camera* cam, int width, int height, d
     return RT_OK;
 }
 
-extern "C" int rt_local_rows(int height, const rt_rows* r, int* out) {
-    if (!out || height < 0) return rt_fail(RT_EINVAL, "rt_local_rows: bad args");
-    if (!r || r->n_ranks <= 1) {
-        if (r && (r->n_ranks < 1 || r->rank != 0)) return rt_fail(RT_EINVAL, "rt_local_rows: bad rank");
-        *out = height;
-        return RT_OK;
-    }
-    if (r->band_height <= 0 || r->rank < 0 || r->rank >= r->n_ranks)
-        return rt_fail(RT_EINVAL, "rt_local_rows: bad band geometry");
+namespace {
+
+int frames_of(const rt_rows* r) { return (r && r->frames > 1) ? r->frames : 1; }
+
+// Rows of one frame that the rank renders.
+int frame_local_rows(int height, const rt_rows* r) {
+    if (!r || r->n_ranks <= 1) return height;
     const int hb = r->band_height, G = r->n_ranks;
     const int full_bands = height / hb, tail = height % hb;
     int n = (full_bands / G) * hb;
-    int extra_bands = full_bands % G;                                           // bands 0..extra-1 of the last round
-    if (r->rank < extra_bands) n += hb;
+    if (r->rank < full_bands % G) n += hb;                                      // bands 0..extra-1 of the last round
     if (tail && (full_bands % G) == r->rank) n += tail;                         // the partial last band
-    *out = n;
+    return n;
+}
+
+}  // namespace
+
+extern "C" int rt_local_rows(int height, const rt_rows* r, int* out) {
+    if (!out || height < 0) return rt_fail(RT_EINVAL, "rt_local_rows: bad args");
+    if (r && (r->frames < 0 || r->n_ranks < 1)) return rt_fail(RT_EINVAL, "rt_local_rows: bad frames / ranks");
+    if (r && r->n_ranks > 1 && (r->band_height <= 0 || r->rank < 0 || r->rank >= r->n_ranks))
+        return rt_fail(RT_EINVAL, "rt_local_rows: bad band geometry");
+    if (r && r->n_ranks == 1 && r->rank != 0) return rt_fail(RT_EINVAL, "rt_local_rows: bad rank");
+    *out = frame_local_rows(height, r) * frames_of(r);
     return RT_OK;
 }
 
@@ -207,13 +215,14 @@ extern "C" int rt_global_row(int height, const rt_rows* r, int local_row, int* o
     int rc = rt_local_rows(height, r, &nl);
     if (rc) return rc;
     if (!out || local_row < 0 || local_row >= nl) return rt_fail(RT_EINVAL, "rt_global_row: row out of range");
-    if (!r || r->n_ranks <= 1) {
-        *out = local_row;
-        return RT_OK;
+    const int per = frame_local_rows(height, r);
+    const int f = local_row / per, lr = local_row % per;
+    int j = lr;
+    if (r && r->n_ranks > 1) {
+        const int hb = r->band_height;
+        j = ((lr / hb) * r->n_ranks + r->rank) * hb + lr % hb;
     }
-    const int hb = r->band_height;
-    const int band = local_row / hb, within = local_row % hb;
-    *out = (band * r->n_ranks + r->rank) * hb + within;
+    *out = f * height + j;
     return RT_OK;
 }
 

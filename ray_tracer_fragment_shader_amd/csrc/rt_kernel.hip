@@ -44,7 +44,9 @@ struct RenderParams {
     double pitch;
     int32_t bottom_x, bottom_y;
     int32_t width, height;
-    int32_t local_rows;
+    int32_t local_rows;                        // over all frames
+    int32_t frame_rows;                        // local rows per frame
+    int32_t frames;
     int32_t band_height, n_ranks, rank;
     int32_t lds_bytes;
     int32_t np;
@@ -52,7 +54,9 @@ struct RenderParams {
     int32_t pad;
 };
 
+// Image row (within its frame) of local row lr; local rows are frame-major (rt_rows.frames).
 __device__ __forceinline__ int global_row_of(const RenderParams& P, int lr) {
+    if (P.frames > 1) lr %= P.frame_rows;
     if (P.n_ranks <= 1) return lr;
     int band = lr / P.band_height, within = lr - band * P.band_height;
     return (band * P.n_ranks + P.rank) * P.band_height + within;
@@ -399,6 +403,8 @@ static int render_params(const rt_ctx* c, const rt_camera* cam, int W, int H, in
     P->band_height = banded ? rows->band_height : H;
     P->n_ranks = banded ? rows->n_ranks : 1;
     P->rank = banded ? rows->rank : 0;
+    P->frames = (rows && rows->frames > 1) ? rows->frames : 1;
+    P->frame_rows = nl / P->frames;
     P->lds_bytes = c->lds_bytes;
     P->np = c->n_padded;
     P->nl = c->n_lights;

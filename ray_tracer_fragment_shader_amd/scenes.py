@@ -232,9 +232,9 @@ PINNED_RAYS = {"c1": 380_817, "c2": 3_684_271, "c3": 18_956_255, "c5": 90_722_78
                "demo": 358_434}
 
 
-def rows(band_height: int = 1, n_ranks: int = 1, rank: int = 0) -> abi.rt_rows:
+def rows(band_height: int = 1, n_ranks: int = 1, rank: int = 0, frames: int = 1) -> abi.rt_rows:
     r = abi.rt_rows()
-    r.band_height, r.n_ranks, r.rank = band_height, n_ranks, rank
+    r.band_height, r.n_ranks, r.rank, r.frames = band_height, n_ranks, rank, frames
     return r
 
 

@@ -67,3 +67,54 @@ def test_band_plan_balances_rows():
         assert sum(p.local) == H
         assert max(p.local) - min(p.local) <= hb
         assert p.slab_rows == max(p.local)
+
+
+def _stream_worker(rank, world, port, W, H, out_prefix):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import pyoracle as po
+        from ray_tracer_fragment_shader_amd import scenes
+        from ray_tracer_fragment_shader_amd.distributed import BandPlan, assemble_on_host, exchange_frames
+
+        cfg = scenes.CONFIGS["c2"]
+        plan = BandPlan(H, world, frames=world)
+        assert plan.balanced
+        rgb, _ = po.render(cfg.scene().to_abi(), cfg.camera(W, H), W, H, cfg.depth, rows=plan.rows(rank),
+                           nthreads=1)
+        fl = plan.frame_local[rank]
+        assert rgb.shape[0] == world * fl                  # frame-major: this rank's bands of every frame
+        local = torch.from_numpy(rgb).reshape(world, fl, W, 3).contiguous()
+        recv = torch.empty_like(local)
+        exchange_frames(local, recv, world)
+        img = assemble_on_host([recv[q].numpy() for q in range(world)], plan)
+        np.save(f"{out_prefix}_{rank}.npy", img)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_frame_streams_all_to_all(tmp_path, world):
+    """Weak-scaling bench layout: every rank ends up with a complete frame assembled from all ranks' bands."""
+    from oracle import pyoracle as po
+    from ray_tracer_fragment_shader_amd import scenes
+
+    W, H = 80, 72
+    prefix = str(tmp_path / "frame")
+    mp.spawn(_stream_worker, args=(world, _free_port(), W, H, prefix), nprocs=world, join=True)
+    cfg = scenes.CONFIGS["c2"]
+    want, _ = po.render(cfg.scene().to_abi(), cfg.camera(W, H), W, H, cfg.depth)
+    for r in range(world):
+        assert np.array_equal(np.load(f"{prefix}_{r}.npy"), want)
+
+
+def test_auto_band_height_balances_bench_sizes():
+    from ray_tracer_fragment_shader_amd.distributed import BandPlan, auto_band_height
+    for H in (480, 1080, 2160, 4320):
+        for N in (1, 2, 4, 8):
+            p = BandPlan(H, N, frames=N)
+            assert p.balanced, (H, N, p.band_height)
+            assert sum(p.frame_local) == H and p.local[0] == N * p.frame_local[0]
+    assert 1080 % (auto_band_height(1080, 8) * 8) == 0

@@ -329,3 +329,22 @@ def test_cli_demo_ppm(tmp_path):
     cfg = scenes.CONFIGS["demo"]
     want, _ = po.render(cfg.scene().to_abi(), cfg.camera(), cfg.width, cfg.height, cfg.depth)
     assert np.array_equal(_read_ppm(out), _ppm_expect(want))
+
+
+@pytest.mark.parametrize("G,frames", [(2, 2), (4, 4), (3, 2)])
+def test_stacked_frames_frame_major(tr, G, frames):
+    """rt_rows.frames: a rank's bands of several frames in one launch, frame-major (the bench's frame
+    streams); every frame's rows equal the single-frame render's."""
+    from ray_tracer_fragment_shader_amd.distributed import BandPlan
+    cfg = scenes.CONFIGS["c2"]
+    W, H = 96, 72
+    full, _ = _render64(tr, cfg.scene(), cfg.camera(W, H), W, H, cfg.depth)
+    plan = BandPlan(H, G, frames=frames)
+    for r in range(G):
+        part, rc = _render64(tr, cfg.scene(), cfg.camera(W, H), W, H, cfg.depth, rows=plan.rows(r))
+        want, want_rc = po.render(cfg.scene().to_abi(), cfg.camera(W, H), W, H, cfg.depth, rows=plan.rows(r))
+        _assert_parity(part, want)
+        fl = plan.frame_local[r]
+        js = [j for j in range(H) if (j // plan.band_height) % G == r]
+        for f in range(frames):
+            assert np.array_equal(part[f * fl:(f + 1) * fl], full[js])
