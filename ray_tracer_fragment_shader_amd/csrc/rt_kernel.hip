@@ -51,7 +51,7 @@ struct RenderParams {
     int32_t lds_bytes;
     int32_t np;
     int32_t nl;
-    int32_t pad;
+    int32_t wg_staging;                        // 1: stage the 32 x 8 tile in LDS behind a workgroup barrier
 };
 
 // Image row (within its frame) of local row lr; local rows are frame-major (rt_rows.frames).
@@ -121,6 +121,18 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
         col = trace<B, true, TRANSP>(V, eye, sp, bdP, dot(bdP, bdP), &seg, &sh);
     }
 
+    if (!P.wg_staging) {
+        // Direct stores: each wave writes its 8 x 8 block as 8 row segments (128 B of RGBA32F each) and
+        // retires without waiting at a workgroup barrier for slower waves of the tile.
+        if (valid) {
+            const size_t k = (size_t)lr * P.width + i;
+            if (out32) out32[k] = make_float4((float)col.x, (float)col.y, (float)col.z, 1.0f);
+            if (out64) { out64[3 * k] = col.x; out64[3 * k + 1] = col.y; out64[3 * k + 2] = col.z; }
+            if (outrc) outrc[k] = seg | (sh << 16);
+            if (out8) out8[k] = make_uchar4(to_u8(col.x), to_u8(col.y), to_u8(col.z), 255);
+        }
+        return;
+    }
     // Stage through LDS, then store whole tile rows.
     const int slot = cy * kTileW + cx;
     if (out32) st32[slot] = make_float4((float)col.x, (float)col.y, (float)col.z, 1.0f);
@@ -297,6 +309,7 @@ struct rt_ctx {
     int min_waves = 5;                         // __launch_bounds__(256, 5) for depth <= 3 (measured faster
                                                // despite small spills: tools/ab.py); RT_MIN_WAVES=0 disables
     int use_lds = 0;                           // RT_SCENE_IN_LDS=1: header + exact records in LDS (A/B: tools/ab.py)
+    int wg_staging = 0;                        // RT_WG_STAGING=1: LDS-staged 32-pixel row stores (A/B)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -330,6 +343,7 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     c->device = device;
     if (const char* e = getenv("RT_SCENE_IN_LDS")) c->use_lds = atoi(e) != 0;
     if (const char* e = getenv("RT_MIN_WAVES")) c->min_waves = atoi(e);
+    if (const char* e = getenv("RT_WG_STAGING")) c->wg_staging = atoi(e) != 0;
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         delete c;
         return rt_fail(RT_EHIP, "rt_ctx_create: hipEventCreate failed");
@@ -408,6 +422,7 @@ static int render_params(const rt_ctx* c, const rt_camera* cam, int W, int H, in
     P->lds_bytes = c->lds_bytes;
     P->np = c->n_padded;
     P->nl = c->n_lights;
+    P->wg_staging = c->wg_staging;
     return RT_OK;
 }
 

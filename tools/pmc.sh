@@ -1,6 +1,7 @@
 #!/bin/bash
 # PMC passes for the dominant kernel (one counter group per rocprofv3 run, --kernel-trace only beside
 # --pmc, as MI355X_MICROARCH.md / the pool rules require).  Usage: CONFIG=c2 bash tools/pmc.sh
+# PMC_GROUPS='A B;C D' overrides the counter groups (';' separates passes).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -15,7 +16,7 @@ while read -r group; do
      python3 "$ROOT/bench.py" --config ${CONFIG:-c2} --steps 10 --warmup 2 --profile-kernel-only \
      > "$OUT/p$i.log" 2>&1 || { echo "pass $i ($group) failed rc=$?"; tail -5 "$OUT/p$i.log"; exit 5; }
   echo "pass $i ok: $group"
-done <<'GROUPS'
+done < <(if [ -n "${PMC_GROUPS:-}" ]; then echo "$PMC_GROUPS" | tr ';' '\n'; else cat <<'GROUPS'
 WRITE_SIZE
 FETCH_SIZE
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
@@ -23,4 +24,5 @@ SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_
 VALUUtilization VALUBusy
 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_WR
 GROUPS
+fi)
 python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/summary.json" && cat "$OUT/summary.json"
