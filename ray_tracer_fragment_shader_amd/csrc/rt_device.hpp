@@ -506,12 +506,15 @@ __device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 
 // materials opaque, no meshes, w = (1,1,1) (multiplication by 1.0 is exact) and any-hit shadows.
 // PRIMARY: p0 is the camera and V.prim/V.primf hold its per-sphere data; (bdP, bdd) = bc - eye, |.|^2.
 // seg / shadow count the rays actually traced.
+// The bounce loop is not unrolled and the per-level colours local[k] (and, TRANSP, the level's material
+// for w[k]) wait in LDS until the right-nested sum, not in registers: slot[(3k + c) kSlotStride],
+// mslot[k kSlotStride], component-major so a wave's 64 lanes touch 64 consecutive words.
+constexpr int kSlotStride = 256;
+
 template <int B, bool PRIMARY, bool TRANSP>
 __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, double bdd, uint32_t* seg,
-                                    uint32_t* shadow) {
+                                    uint32_t* shadow, double* slot, int* mslot) {
     const DevScene* S = V.S;
-    d3 local[B + 1];
-    d3 wgt[TRANSP ? B + 1 : 1];
     int levels = 0;
     Ray r;
     r.p0 = p0;
@@ -520,8 +523,6 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
     uint32_t nseg = 0, nsh = 0;
 #pragma unroll
     for (int lvl = 0; lvl <= B; ++lvl) {
-        local[lvl] = mk(0.0, 0.0, 0.0);
-        if (TRANSP) wgt[lvl] = mk(1.0, 1.0, 1.0);
         bool alive = lvl == 0 || levels == lvl;
         if (!__any(alive)) break;                           // the whole wave has missed: early out
         if (alive) {
@@ -540,7 +541,11 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                 surface(V, kind, p, r.u, &n, &mat, &pe);
                 d3 rd = sub(pe, p);                         // reflectedRay = Line(p, p + r)
                 d3 rdir = divs(rd, len(rd));                // reflectedRay.direction()
-                local[lvl] = shade<TRANSP>(V, p, n, mat, r.u, rdir);
+                d3 c = shade<TRANSP>(V, p, n, mat, r.u, rdir);
+                double* sl = slot + 3 * lvl * kSlotStride;
+                sl[0] = c.x;
+                sl[kSlotStride] = c.y;
+                sl[2 * kSlotStride] = c.z;
                 nsh += V.nl;
                 levels = lvl + 1;
                 r.p0 = p;                                   // the next level traces the continuation
@@ -551,17 +556,17 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                 } else {
                     set_dir(&r, rd, rdir);
                 }
-                if (TRANSP) wgt[lvl] = ld3(S->mat[mat].w);
+                if (TRANSP) mslot[lvl * kSlotStride] = mat;
             }
         }
     }
     d3 acc = mk(0.0, 0.0, 0.0);
-#pragma unroll
-    for (int lvl = B; lvl >= 0; --lvl) {
-        if (lvl < levels) {
-            if (lvl == levels - 1) acc = local[lvl];
-            else acc = TRANSP ? add(local[lvl], had(wgt[lvl], acc)) : add(local[lvl], acc);
-        }
+#pragma unroll 1
+    for (int lvl = levels - 1; lvl >= 0; --lvl) {
+        const double* sl = slot + 3 * lvl * kSlotStride;
+        d3 c = mk(sl[0], sl[kSlotStride], sl[2 * kSlotStride]);
+        if (lvl == levels - 1) acc = c;
+        else acc = TRANSP ? add(c, had(ld3(S->mat[mslot[lvl * kSlotStride]].w), acc)) : add(c, acc);
     }
     *seg = nseg;
     *shadow = nsh;

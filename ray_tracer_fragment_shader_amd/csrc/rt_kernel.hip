@@ -35,6 +35,12 @@ namespace {
 constexpr int kTileW = 32;   // workgroup tile: 32 columns ...
 constexpr int kTileH = 8;    // ... x 8 rows = 256 pixels
 constexpr int kThreads = 256;
+static_assert(kThreads == kSlotStride, "one LDS colour slot column per work-item");
+
+// LDS bytes of trace()'s per-level slots for depth B: 3 doubles (+ the material id when TRANSP) per level.
+__host__ __device__ constexpr int slot_bytes(int B, bool transp) {
+    return (B + 1) * (3 * 8 + (transp ? 4 : 0)) * kSlotStride;
+}
 
 struct RenderParams {
     double eye[3];
@@ -82,7 +88,8 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
                                                              uint32_t* __restrict__ outrc) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
-    // LDS: [header | DevSphere[np] | DevSpherePrim[np]] (LDS = 1) then the output staging tile (12 KB).
+    // LDS: [header | DevSphere[np] | DevSpherePrim[np]] (LDS = 1), the per-level colour slots of trace()
+    // (slot_bytes), then the output staging tile (12 KB, RT_WG_STAGING only).
     // The scene record is broadcast into LDS once per workgroup; the FP32 filter images stay in global
     // memory and are read with wave-uniform indices (scalar loads, SGPR operands).
     int off = 0;
@@ -92,6 +99,9 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
         S = reinterpret_cast<const DevScene*>(smem);
         off = P.lds_bytes;
     }
+    double* slot = reinterpret_cast<double*>(smem + off) + tid;
+    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * (B + 1) * kSlotStride) + tid;
+    off += slot_bytes(B, TRANSP);
     float4* st32 = reinterpret_cast<float4*>(smem + off);                              // [8][32] 4 KB
     double* st64 = reinterpret_cast<double*>(smem + off + 4096);                        // [8][32][3] 6 KB
     uint32_t* strc = reinterpret_cast<uint32_t*>(smem + off + 4096 + 6144);             // [8][32] 1 KB
@@ -118,7 +128,7 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
         d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(i + P.bottom_x), right)),
                     scl(P.pitch * (double)(j + P.bottom_y), upp));
         d3 bdP = sub(ld3(V.S->bc), eye);           // bounding-sphere deltaP for p0 = camera
-        col = trace<B, true, TRANSP>(V, eye, sp, bdP, dot(bdP, bdP), &seg, &sh);
+        col = trace<B, true, TRANSP>(V, eye, sp, bdP, dot(bdP, bdP), &seg, &sh, slot, mslot);
     }
 
     if (!P.wg_staging) {
@@ -134,11 +144,11 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
         return;
     }
     // Stage through LDS, then store whole tile rows.
-    const int slot = cy * kTileW + cx;
-    if (out32) st32[slot] = make_float4((float)col.x, (float)col.y, (float)col.z, 1.0f);
-    if (out64) { st64[3 * slot] = col.x; st64[3 * slot + 1] = col.y; st64[3 * slot + 2] = col.z; }
-    if (outrc) strc[slot] = seg | (sh << 16);
-    if (out8) st8[slot] = make_uchar4(to_u8(col.x), to_u8(col.y), to_u8(col.z), 255);
+    const int ts = cy * kTileW + cx;
+    if (out32) st32[ts] = make_float4((float)col.x, (float)col.y, (float)col.z, 1.0f);
+    if (out64) { st64[3 * ts] = col.x; st64[3 * ts + 1] = col.y; st64[3 * ts + 2] = col.z; }
+    if (outrc) strc[ts] = seg | (sh << 16);
+    if (out8) st8[ts] = make_uchar4(to_u8(col.x), to_u8(col.y), to_u8(col.z), 255);
     __syncthreads();
     const int oy = tid >> 5, ox = tid & 31;
     const int gi = tx * kTileW + ox, glr = ty * kTileH + oy;
@@ -192,11 +202,15 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
                                                                  const double* __restrict__ ends, int n,
                                                                  double* __restrict__ rgb,
                                                                  uint32_t* __restrict__ rc) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     const int k = blockIdx.x * kThreads + threadIdx.x;
     if (k >= n) return;
     uint32_t seg = 0, sh = 0;
     const SceneView V = view_of(S, S, S->n_padded, S->n_lights);
-    d3 c = trace<B, false, TRANSP>(V, ld3(starts + 3 * k), ld3(ends + 3 * k), mk(0.0, 0.0, 0.0), 0.0, &seg, &sh);
+    double* slot = reinterpret_cast<double*>(smem) + threadIdx.x;
+    int* mslot = reinterpret_cast<int*>(smem + 3 * 8 * (B + 1) * kSlotStride) + threadIdx.x;
+    d3 c = trace<B, false, TRANSP>(V, ld3(starts + 3 * k), ld3(ends + 3 * k), mk(0.0, 0.0, 0.0), 0.0, &seg, &sh,
+                                   slot, mslot);
     if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
     if (rc) rc[k] = seg | (sh << 16);
 }
@@ -278,8 +292,8 @@ hipError_t launch_trace_rays(int depth, dim3 grid, hipStream_t st, const DevScen
                              const double* b, int n, double* rgb, uint32_t* rc) {
 #define RT_CASE(k)                                                                                      \
     case k:                                                                                             \
-        hipLaunchKernelGGL((rt_trace_rays_kernel<k, TRANSP>), grid, dim3(kThreads), 0, st, s, a, b, n, rgb,\
-                           rc);                                                                         \
+        hipLaunchKernelGGL((rt_trace_rays_kernel<k, TRANSP>), grid, dim3(kThreads), slot_bytes(k, TRANSP), st, s, \
+                           a, b, n, rgb, rc);                                                           \
         break;
     switch (depth) {
         RT_CASE(0) RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7)
@@ -436,7 +450,7 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     const int tiles_x = (W + kTileW - 1) / kTileW;
     const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
     dim3 grid((unsigned)(tiles_x * tiles_y));
-    const size_t stage = 4096 + 6144 + 1024 + 1024;
+    const size_t stage = (c->wg_staging ? 4096 + 6144 + 1024 + 1024 : 0) + slot_bytes(depth, c->transparent);
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     // Primary-ray sphere data for this eye (stream-ordered; only when the eye changes).
