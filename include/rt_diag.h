@@ -1,0 +1,26 @@
+/*
+ * rt_diag.h — diagnostics exported by librt_amd.so beside the drop-in boundary (rt_api.h).
+ *
+ * Not part of the reference's interface: these entry points exist so the parity tests can check the
+ * device arithmetic the render kernel relies on, operand by operand, against the compiler's IEEE
+ * sequences (and, on the host, against binary64 arithmetic as the reference's Point does it,
+ * Hw4/MySdlApplication.cpp:174-175).
+ */
+#ifndef RT_DIAG_H
+#define RT_DIAG_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* op 0: for each of n vectors v (3 doubles, device memory) write 9 doubles (device memory):
+ *   [0..2] v / |v| and [3] |v| with the compiler's sqrt and division (Point::normalize / length),
+ *   [4..7] the same from the render kernel's fast path (unit), [8] its len_fast(v).
+ * Asynchronous on `stream`.  RT_EINVAL for an unknown op or null buffers. */
+int rt_probe_math_dev(int op, const double* in, int n, double* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_DIAG_H */

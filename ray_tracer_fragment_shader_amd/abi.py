@@ -121,6 +121,8 @@ SIGNATURES = {
     "rt_trace_rays_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "rt_unshuffle_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "rt_write_ppm": (c_int, [c_char_p, _P(c_uint8), c_int, c_int, c_int]),
+    # include/rt_diag.h
+    "rt_probe_math_dev": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p]),
 }
 
 _lib = None

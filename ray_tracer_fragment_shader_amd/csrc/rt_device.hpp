@@ -45,6 +45,84 @@ __device__ __forceinline__ double len(d3 a) { return sqrt(a.x * a.x + a.y * a.y 
 __device__ __forceinline__ d3 divs(d3 a, double l) { return mk(a.x / l, a.y / l, a.z / l); }      // :175
 __device__ __forceinline__ d3 ld3(const double* p) { return mk(p[0], p[1], p[2]); }
 
+// ------------------------------------------------------------------------------------------------
+// Exact fast paths for |v| and v / |v|.
+// The compiler lowers IEEE sqrt and division on gfx950 to these sequences (lib/isa/rt_kernel.s):
+//   sqrt(x): x < 2^-767 is scaled by 2^256; y = rsq(x); g = x y; h = y / 2; r = fma(-h, g, 1/2);
+//            g = fma(g, r, g); d = fma(-g, g, x); h = fma(h, r, h); g = fma(d, h, g); d = fma(-g, g, x);
+//            g = fma(d, h, g); unscale; x in {+0, -0, +inf} returns x.
+//   a / b:   b' = div_scale(b); r = rcp(b'); e = fma(-b', r, 1); r = fma(r, e, r); e = fma(-b', r, 1);
+//            r = fma(r, e, r); a' = div_scale(a); q = a' r; e = fma(-b', q, a'); q = div_fmas(e, r, q);
+//            div_fixup(q, b, a).
+// For operands away from the scaling and special-value thresholds the scale, class and fixup steps are
+// identities (fixup returns |q| with the sign of a XOR b; for a = +-0 it returns that signed zero), so
+// the remaining operations, run here explicitly, give the same bits.  Each fast path checks its
+// operands and takes the compiler's sequence otherwise:
+//   sqrt_core: 2^-700 <= x <= 2^700 (no scaling: x >= 2^-767; finite, nonzero);
+//   unit():    s = |v|^2 in [2^-700, 2^700], so l = sqrt(s) in [2^-350, 2^350] (l and 1/l normal), and
+//              every component 0 or |v_i| >= 2^-500 (no numerator scaling: |v_i| >= 2^-969, quotient
+//              >= 2^-850 normal, |v_i| <= l (1 + 2^-50) so exponent(v_i) - exponent(l) <= 1 < 768).
+//              The three quotients share the reciprocal r (it depends on b only) — the compiler emits
+//              it three times — and l > 0 makes the fixup's sign that of v_i (copysign).
+// tests/test_gpu_parity.py::test_math_fast_paths checks both against the compiler's sqrt and division
+// (and numpy's binary64) on adversarial operands through rt_probe_math_dev (include/rt_diag.h).
+__device__ __forceinline__ double sqrt_core(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    double d = fma(-g, g, x);
+    h = fma(h, r, h);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    return fma(d, h, g);
+}
+
+__device__ __forceinline__ bool sqrt_fast_ok(double x) { return x >= 0x1p-700 && x <= 0x1p+700; }
+
+__device__ __forceinline__ double rcp_core(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    double e = fma(-b, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-b, r, 1.0);
+    return fma(r, e, r);
+}
+
+__device__ __forceinline__ double div_core(double a, double b, double r) {
+    double q = a * r;
+    double e = fma(-b, q, a);
+    return fma(e, r, q);
+}
+
+__device__ __forceinline__ bool num_fast_ok(double a) { return a == 0.0 || fabs(a) >= 0x1p-500; }
+
+// |a| (= len(a), :174).
+__device__ __forceinline__ double len_fast(d3 a) {
+    double s = a.x * a.x + a.y * a.y + a.z * a.z;
+    return sqrt_fast_ok(s) ? sqrt_core(s) : sqrt(s);
+}
+
+// u = a / |a| component-wise (= divs(a, len(a)), :174-175, Line::direction :258-263); *l = |a|.
+__device__ __forceinline__ d3 unit(d3 a, double* l) {
+    double s = a.x * a.x + a.y * a.y + a.z * a.z;
+    if (sqrt_fast_ok(s) && num_fast_ok(a.x) && num_fast_ok(a.y) && num_fast_ok(a.z)) {
+        double L = sqrt_core(s);
+        double r = rcp_core(L);
+        *l = L;
+        return mk(copysign(div_core(a.x, L, r), a.x), copysign(div_core(a.y, L, r), a.y),
+                  copysign(div_core(a.z, L, r), a.z));
+    }
+    double L = sqrt(s);
+    *l = L;
+    return divs(a, L);
+}
+
+__device__ __forceinline__ d3 unit(d3 a) {
+    double l;
+    return unit(a, &l);
+}
+
 // Where the kernels read the scene from.  `S`, `sph`, `prim` (header and FP64 exact records) live in
 // LDS in the render kernel (or in global memory for the ray-list kernels); the FP32 filter images `sphf`,
 // `primf` are always read from global memory with wave-uniform indices, i.e. through the scalar cache
@@ -219,7 +297,7 @@ __device__ __forceinline__ int mesh_closest_tri(const SceneView& V, const DevMes
             h = tri_hit(V.tri[t], p0, d, eps, &q);
         }
         if (h) {
-            double dist = len(sub(q, p0));
+            double dist = len_fast(sub(q, p0));
             if (dist < *mbest || *mbest < 0.0) {
                 *mbest = dist;
                 mt = t;
@@ -309,7 +387,7 @@ __device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const R
         pass &= pass - 1;
         d3 q;
         if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) {
-            double dist = len(sub(q, r.p0));                // :811-812
+            double dist = len_fast(sub(q, r.p0));                // :811-812
             if (dist < *best || *best < 0.0) {              // :813
                 *best = dist;
                 *kind = 1 + k;
@@ -329,7 +407,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
         d3 q;
         if (board_hit(S, r.p0, r.d, &q)) {
             kind = 0;
-            best = len(sub(q, r.p0));
+            best = len_fast(sub(q, r.p0));
             *hp = q;
         }
     }
@@ -352,7 +430,7 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
         d3 q;
         if (board_hit(S, r.p0, r.d, &q)) {
             kind = 0;
-            best = len(sub(q, r.p0));
+            best = len_fast(sub(q, r.p0));
             *hp = q;
         }
     }
@@ -373,7 +451,7 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
             const DevSpherePrim& pp = V.prim[k];
             d3 q;
             if (sphere_hit_dp(ld3(pp.dP), pp.dd, V.sph[k].r2, r.p0, r.u, eps, &q)) {
-                double dist = len(sub(q, r.p0));
+                double dist = len_fast(sub(q, r.p0));
                 if (dist < best || best < 0.0) {
                     best = dist;
                     kind = 1 + k;
@@ -463,7 +541,7 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
     } else {
         d3 c = ld3(V.sph[kind - 1].c);
         d3 dp = sub(p, c);                                  // directionP0 (:763)
-        *n = divs(dp, len(dp));                             // :774-775
+        *n = unit(dp);                                      // :774-775
     }
     *mat = material_of(V, kind, p);
     d3 r = sub(u, scl(2 * dot(u, *n), *n));                 // :682 / :777
@@ -486,8 +564,8 @@ __device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 
     for (int i = 0; i < V.nl; ++i) {
         d3 lpos = ld3(S->light[i].pos);
         d3 sd = sub(lpos, p);                               // shadowRay end - start (:1216)
-        double dl = len(sd);                                // shadowRay.length()
-        d3 sdir = divs(sd, dl);                             // shadowRay.direction()
+        double dl;                                          // shadowRay.length()
+        d3 sdir = unit(sd, &dl);                            // shadowRay.direction()
         set_dir(&sr, sd, sdir);
         if (!(FULL ? occluded_transparent(V, sr) : occluded<false>(V, sr))) {
             double a = S->att / (S->att + dl * dl);         // attenuation (:1181)
@@ -519,7 +597,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
     Ray r;
     r.p0 = p0;
     d3 d = sub(p1, p0);
-    set_dir(&r, d, divs(d, len(d)));
+    set_dir(&r, d, unit(d));
     uint32_t nseg = 0, nsh = 0;
 #pragma unroll
     for (int lvl = 0; lvl <= B; ++lvl) {
@@ -540,7 +618,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                 int mat;
                 surface(V, kind, p, r.u, &n, &mat, &pe);
                 d3 rd = sub(pe, p);                         // reflectedRay = Line(p, p + r)
-                d3 rdir = divs(rd, len(rd));                // reflectedRay.direction()
+                d3 rdir = unit(rd);                         // reflectedRay.direction()
                 d3 c = shade<TRANSP>(V, p, n, mat, r.u, rdir);
                 double* sl = slot + 3 * lvl * kSlotStride;
                 sl[0] = c.x;
@@ -552,7 +630,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                 if (TRANSP && S->mat[mat].transmit) {
                     d3 pt = transmitted_end(V, kind, mat, p, r.u, n);
                     d3 td = sub(pt, p);                     // transmittedRay = Line(p, p + t)
-                    set_dir(&r, td, divs(td, len(td)));
+                    set_dir(&r, td, unit(td));
                 } else {
                     set_dir(&r, rd, rdir);
                 }

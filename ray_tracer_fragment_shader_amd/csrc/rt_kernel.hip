@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/rt_api.h"
+#include "../../include/rt_diag.h"
 #include "rt_device.hpp"
 #include "rt_internal.hpp"
 
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void rt_intersect_kernel(const DevScene* 
     Ray r;
     r.p0 = ld3(starts + 3 * k);
     d3 d = sub(ld3(ends + 3 * k), r.p0);
-    set_dir(&r, d, divs(d, len(d)));
+    set_dir(&r, d, unit(d));
     set_origin_f32(S, &r);
     d3 p;
     int kind = closest_hit<true>(V, r, &p);
@@ -262,6 +263,24 @@ __global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* 
     const uint32_t* s = src + ((size_t)rank * slab_rows + lr) * row_words;
     uint32_t* d = dst + (size_t)j * row_words;
     for (int w = threadIdx.x; w < row_words; w += kThreads) d[w] = s[w];
+}
+
+// Diagnostics (include/rt_diag.h): the exact-arithmetic fast paths of rt_device.hpp beside the compiler's
+// IEEE sequences, on caller-supplied operands.  op 0: per vector v (3 doubles) -> 9 doubles
+// [divs(v, len(v)), len(v), unit(v), |v| from unit(), len_fast(v)].
+__global__ __launch_bounds__(kThreads) void rt_probe_math_kernel(int op, const double* __restrict__ in, int n,
+                                                                 double* __restrict__ out) {
+    const int k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= n || op != 0) return;
+    const d3 v = mk(in[3 * k], in[3 * k + 1], in[3 * k + 2]);
+    double* o = out + 9 * (size_t)k;
+    const double l0 = len(v);
+    const d3 u0 = divs(v, l0);
+    double l1;
+    const d3 u1 = unit(v, &l1);
+    o[0] = u0.x, o[1] = u0.y, o[2] = u0.z, o[3] = l0;
+    o[4] = u1.x, o[5] = u1.y, o[6] = u1.z, o[7] = l1;
+    o[8] = len_fast(v);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -578,5 +597,16 @@ extern "C" int rt_unshuffle_dev(const void* gathered, void* image, int W, int H,
                        (const uint32_t*)gathered, (uint32_t*)image, row_words, H, band_height, n_ranks, slab_rows);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_unshuffle_kernel: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+extern "C" int rt_probe_math_dev(int op, const double* in, int n, double* out, void* stream) {
+    if (op != 0) return rt_fail(RT_EINVAL, "rt_probe_math_dev: unknown op");
+    if (n < 0 || (n > 0 && (!in || !out))) return rt_fail(RT_EINVAL, "rt_probe_math_dev: bad buffers");
+    if (n == 0) return RT_OK;
+    hipLaunchKernelGGL(rt_probe_math_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                       (hipStream_t)stream, op, in, n, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_probe_math_kernel: ") + hipGetErrorString(e));
     return RT_OK;
 }

@@ -10,18 +10,20 @@ import pytest
 from ray_tracer_fragment_shader_amd import abi, scenes
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "rt_api.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("rt_api.h", "rt_diag.h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(rt_[a-z_0-9]+)\s*\(", src, flags=re.M)))
+    names = set()
+    for h in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(rt_[a-z_0-9]+)\s*\(", src, flags=re.M))
+    return sorted(names)
 
 
 def test_every_declared_symbol_is_exported():
     names = declared_functions()
-    assert len(names) >= 19
+    assert len(names) >= 20 and "rt_probe_math_dev" in names
     L = abi.lib()
     for n in names:
         assert hasattr(L, n), n

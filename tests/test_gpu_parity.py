@@ -348,3 +348,51 @@ def test_stacked_frames_frame_major(tr, G, frames):
         js = [j for j in range(H) if (j // plan.band_height) % G == r]
         for f in range(frames):
             assert np.array_equal(part[f * fl:(f + 1) * fl], full[js])
+
+
+def _math_operands(rng):
+    """Vectors around every threshold of the sqrt / division fast paths (rt_device.hpp)."""
+    vals = [0.0, -0.0, 1.0, -1.0, 3.0, 1e-300, -1e-300, 5e-324, -5e-324, 2.2250738585072014e-308,
+            2.0 ** -500, -(2.0 ** -500), 2.0 ** -501, 2.0 ** -499, 2.0 ** -350, 2.0 ** -351, 2.0 ** -349,
+            2.0 ** 350, 2.0 ** 349.5, 2.0 ** 351, 1e200, 1e300, -1e300, np.inf, -np.inf, np.nan,
+            40.0, 0.1, 1e-14, 160.0, -320.0, 277.12812921102034]
+    vals = np.array(vals)
+    rows = [rng.choice(vals, size=3) for _ in range(4000)]
+    with np.errstate(over="ignore"):
+        big = [(np.ldexp(1.0, e), np.exp2(e / 2)) for e in range(-1100, 1100, 7)]
+    for p, h in big:                                     # one component across the exponent range
+        rows.append(np.array([p, 1.0, 0.0]))
+        rows.append(np.array([h, h * 0.7, -h * 0.3]))
+    rows += list(rng.normal(size=(4000, 3)) * 10.0 ** rng.uniform(-20, 20, size=(4000, 1)))
+    rows += list(rng.uniform(-400, 400, size=(4000, 3)))
+    rows += list(np.where(rng.random((2000, 3)) < 0.3, 0.0, rng.normal(size=(2000, 3))))
+    return np.ascontiguousarray(np.array(rows, dtype=np.float64))
+
+
+def _same_bits(a, b):
+    ia, ib = a.view(np.int64), b.view(np.int64)
+    return (ia == ib) | (np.isnan(a) & np.isnan(b))
+
+
+def test_math_fast_paths(tr):
+    """unit()/len_fast() (exact fast paths of the render kernel) return the bits of the compiler's IEEE
+    sqrt and division, which are the binary64 results numpy computes on the host."""
+    import torch
+    v = _math_operands(np.random.default_rng(7))
+    n = len(v)
+    dv = torch.from_numpy(v).cuda()
+    out = torch.empty((n, 9), dtype=torch.float64, device="cuda")
+    abi.check(abi.lib().rt_probe_math_dev(0, ctypes.c_void_p(dv.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
+                                          None), "rt_probe_math_dev")
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    with np.errstate(all="ignore"):
+        s = (v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1]) + v[:, 2] * v[:, 2]
+        l = np.sqrt(s)
+        u = v / l[:, None]
+    assert _same_bits(o[:, 3], l).all()
+    assert _same_bits(o[:, 0:3], u).all()
+    assert _same_bits(o[:, 4:8], o[:, 0:4]).all()
+    assert _same_bits(o[:, 8], o[:, 3]).all()
+    fast = (s >= 2.0 ** -700) & (s <= 2.0 ** 700)
+    assert fast.sum() > n // 2 and (~fast).sum() > 100        # both paths exercised
