@@ -133,6 +133,7 @@ struct SceneView {
     const DevSpherePrim* prim;
     const DevSphereF* sphf;
     const DevSpherePrimF* primf;
+    const DevSphereLightF* lightf;   // [nl][np] shadow-ray cone filter
     const DevMesh* mesh;             // global, wave-uniform reads
     const DevTri* tri;
     int np;                          // padded sphere count (wave-uniform)
@@ -152,7 +153,8 @@ __device__ __forceinline__ SceneView view_of(const DevScene* hdr, const DevScene
     const DevSpherePrim* gprim = reinterpret_cast<const DevSpherePrim*>(gsph + np);
     v.sphf = reinterpret_cast<const DevSphereF*>(gprim + np);
     v.primf = reinterpret_cast<const DevSpherePrimF*>(v.sphf + np);
-    v.mesh = reinterpret_cast<const DevMesh*>(v.primf + np);
+    v.lightf = reinterpret_cast<const DevSphereLightF*>(v.primf + np);
+    v.mesh = reinterpret_cast<const DevMesh*>(v.lightf + (size_t)nl * np);
     v.nm = g->n_meshes;
     v.tri = reinterpret_cast<const DevTri*>(v.mesh + v.nm);
     return v;
@@ -465,15 +467,28 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
 }
 
 // Shadow test: intersects() of g_scene.intersection(Line(pt, Lpos)) (:1216-1221), any hit.
+// Spheres are filtered with the light's cone records: the ray lies on a line through light `li`, which
+// meets sphere k only if |u . v_k| >= cos(phi_k) (host builder, rt_host.cpp).  FP32 error of the lane's
+// dot product: |f32(u) - u|, |f32(v_k) - v_k| <= sqrt(3) 2^-24 and three roundings, < 7 * 2^-24 in all,
+// far inside the 2^-16 folded into c_k; the FP64 hit test's own rounding moves the line by ~1e-13
+// relative, likewise covered.  A NaN direction is not rejected (it compares false), as the FP64 test
+// reports NaN rays as hits.
 template <bool FULL>
-__device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r) {
+__device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li) {
     const DevScene* S = V.S;
     if (!bound_pass(S, r.p0, r.u)) return false;
     const double eps = S->eps;
+    const DevSphereLightF* lf = V.lightf + li * V.np;
     for (int k0 = 0; k0 < V.np; k0 += kChunk) {
         uint32_t pass = 0;
 #pragma unroll
-        for (int j = 0; j < kChunk; ++j) pass |= (sphere_reject32(V.sphf[k0 + j], r) ? 0u : 1u) << j;
+        for (int j = 0; j < kChunk; ++j) {
+            const DevSphereLightF& f = lf[k0 + j];
+            float t = r.ux * f.vx;
+            t = fmaf(r.uy, f.vy, t);
+            t = fmaf(r.uz, f.vz, t);
+            pass |= (fabsf(t) < f.c ? 0u : 1u) << j;
+        }
         while (pass) {
             const int k = k0 + __builtin_ctz(pass);
             pass &= pass - 1;
@@ -560,14 +575,14 @@ __device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 
     d3 color = mk(0.0, 0.0, 0.0);
     Ray sr;
     sr.p0 = p;
-    set_origin_f32(S, &sr);
+    if (FULL) set_origin_f32(S, &sr);                       // closest-hit shadows use the ray filter
     for (int i = 0; i < V.nl; ++i) {
         d3 lpos = ld3(S->light[i].pos);
         d3 sd = sub(lpos, p);                               // shadowRay end - start (:1216)
         double dl;                                          // shadowRay.length()
         d3 sdir = unit(sd, &dl);                            // shadowRay.direction()
         set_dir(&sr, sd, sdir);
-        if (!(FULL ? occluded_transparent(V, sr) : occluded<false>(V, sr))) {
+        if (!(FULL ? occluded_transparent(V, sr) : occluded<false>(V, sr, i))) {
             double a = S->att / (S->att + dl * dl);         // attenuation (:1181)
             d3 lC = scl(a, ld3(S->light[i].col));           // :1223
             d3 term = add(add(had(amb, lC), scl(fabs(dot(n, sdir)), had(dif, lC))), scl(ks, had(spc, lC)));

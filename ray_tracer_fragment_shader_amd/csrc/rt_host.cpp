@@ -285,7 +285,7 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
         dm[m].transparent = zeroT ? 0 : 1;
     }
 
-    const size_t bytes = (size_t)rt::scene_bytes_for(s->n_spheres, s->n_meshes, n_tris);
+    const size_t bytes = (size_t)rt::scene_bytes_for(s->n_spheres, s->n_meshes, n_tris, s->n_lights);
     const int np = rt::padded_spheres(s->n_spheres);
     blob->assign(bytes, 0);
     rt::DevScene* d = reinterpret_cast<rt::DevScene*>(blob->data());
@@ -386,10 +386,45 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
         sph[k].r2 = -inf;
         sphf[k].rm = -std::numeric_limits<float>::infinity();
     }
+    // Shadow-ray cone filter (rt_device.hpp occluded): a shadow ray Line(p, L) lies on a line through the
+    // light L, so it can meet sphere k only if |u . v_k| >= cos(phi_k), v_k = unit(C_k - L),
+    // sin(phi_k) = r / |C_k - L|.  Stored: f32(v_k) and c_k = cos(phi_k) - 2^-16 rounded down; a light
+    // inside or near a sphere (|C - L| <= r (1 + 2^-20) or |C - L| <= 2^-14 (1 + |L| + |C|)) gets c = -inf
+    // (always tested), padding spheres c = +inf (never).
+    rt::DevSphereLightF* lightf = reinterpret_cast<rt::DevSphereLightF*>(
+        reinterpret_cast<rt::DevSpherePrimF*>(sphf + np) + np);
+    for (int i = 0; i < s->n_lights; ++i) {
+        const HP L = hp(s->lights[i].position);
+        const double aL = std::max(std::fabs(L.x), std::max(std::fabs(L.y), std::fabs(L.z)));
+        for (int k = 0; k < np; ++k) {
+            rt::DevSphereLightF& f = lightf[i * np + k];
+            f.vx = f.vy = f.vz = 0.0f;
+            if (k >= s->n_spheres) {
+                f.c = std::numeric_limits<float>::infinity();
+                continue;
+            }
+            const HP C = hp(sph[k].c[0], sph[k].c[1], sph[k].c[2]);
+            const HP v = C - L;
+            const double D = length(v), r = std::fabs(s->spheres[k].radius);
+            const double aC = std::max(std::fabs(C.x), std::max(std::fabs(C.y), std::fabs(C.z)));
+            if (!(D > r * (1.0 + 0x1p-20) && D > 0x1p-14 * (1.0 + aL + aC))) {
+                f.c = -std::numeric_limits<float>::infinity();
+                continue;
+            }
+            const double sn = r / D;
+            const double c = std::sqrt(std::max(0.0, 1.0 - sn * sn)) - 0x1p-16;
+            f.vx = (float)(v.x / D);
+            f.vy = (float)(v.y / D);
+            f.vz = (float)(v.z / D);
+            float cf = (float)c;
+            if ((double)cf > c) cf = std::nextafter(cf, -std::numeric_limits<float>::infinity());
+            f.c = cf;
+        }
+    }
     // Meshes (Tetrahedron :863-900, Cube :903-950): Shape(p, m, sqrt(3)*edge/2, false) with Triangle /
     // Quad sub-objects at zero position.  World vertex 0 of a triangle: tetrahedron (zero + (p + bc)) + v0,
     // cube (zero + (zero + (p + bc))) + v0 — the chain of `_position + positionOffset` additions (:739, :640).
-    rt::DevMesh* dmesh = reinterpret_cast<rt::DevMesh*>(reinterpret_cast<rt::DevSpherePrimF*>(sphf + np) + np);
+    rt::DevMesh* dmesh = reinterpret_cast<rt::DevMesh*>(lightf + (size_t)s->n_lights * np);
     rt::DevTri* dtri = reinterpret_cast<rt::DevTri*>(dmesh + s->n_meshes);
     d->n_meshes = s->n_meshes;
     d->n_tris = n_tris;

@@ -5,7 +5,8 @@
 //   DevSphere[np]       FP64 exact data                 ┐ copied into LDS once per workgroup
 //   DevSpherePrim[np]   primary-ray FP64 data (per eye)  ┘ (lds_bytes)
 //   DevSphereF[np]      FP32 filter image               ┐ read through the scalar cache (SGPR operands),
-//   DevSpherePrimF[np]  primary-ray FP32 filter (per eye)┘ one batch of kChunk records per s_load group
+//   DevSpherePrimF[np]  primary-ray FP32 filter (per eye)│ one batch of kChunk records per s_load group
+//   DevSphereLightF[nl][np]  shadow-ray FP32 cone filter ┘ per light (line through the light)
 //   DevMesh[nm]         tetrahedra / cubes: bounding sphere, triangle range, material, child index
 //   DevTri[nt]          their triangles (world vertex 0, u, v, n, uv, uu, vv, den)
 // np = n_spheres rounded up to kChunk; the padding spheres have r2 = -inf and filter terms = -inf, so
@@ -75,6 +76,10 @@ struct alignas(16) DevSpherePrimF {    // FP32 filter for primary rays: f32(dP),
     float dx, dy, dz, c0;
 };
 
+struct alignas(16) DevSphereLightF {   // shadow rays to light i: f32(unit(C - L)) and cos(phi) - margin,
+    float vx, vy, vz, c;               // phi = asin(r / |C - L|); c = -inf: always test, +inf: never (padding)
+};
+
 struct alignas(16) DevScene {
     double bc[3];                      // g_scene position + (0,0,0)                     (:739)
     double br2;                        // g_scene radius squared                          (:750)
@@ -106,8 +111,10 @@ inline constexpr int lds_bytes_for(int n) {
     return (int)(sizeof(DevScene) + (sizeof(DevSphere) + sizeof(DevSpherePrim)) * (unsigned)padded_spheres(n));
 }
 
-inline constexpr int scene_bytes_for(int n, int n_meshes = 0, int n_tris = 0) {
-    return lds_bytes_for(n) + (int)((sizeof(DevSphereF) + sizeof(DevSpherePrimF)) * (unsigned)padded_spheres(n)) +
+inline constexpr int scene_bytes_for(int n, int n_meshes = 0, int n_tris = 0, int n_lights = 0) {
+    return lds_bytes_for(n) +
+           (int)((sizeof(DevSphereF) + sizeof(DevSpherePrimF) + sizeof(DevSphereLightF) * (unsigned)n_lights) *
+                 (unsigned)padded_spheres(n)) +
            (int)(sizeof(DevMesh) * (unsigned)n_meshes + sizeof(DevTri) * (unsigned)n_tris);
 }
 
