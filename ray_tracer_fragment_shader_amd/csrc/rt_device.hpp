@@ -133,6 +133,7 @@ struct SceneView {
     const DevSpherePrim* prim;
     const DevSphereF* sphf;
     const DevSpherePrimF* primf;
+    const DevSphereCone* cone;       // [np] primary-ray cones (per eye)
     const DevSphereLightF* lightf;   // [nl][np] shadow-ray cone filter
     const DevMesh* mesh;             // global, wave-uniform reads
     const DevTri* tri;
@@ -153,7 +154,8 @@ __device__ __forceinline__ SceneView view_of(const DevScene* hdr, const DevScene
     const DevSpherePrim* gprim = reinterpret_cast<const DevSpherePrim*>(gsph + np);
     v.sphf = reinterpret_cast<const DevSphereF*>(gprim + np);
     v.primf = reinterpret_cast<const DevSpherePrimF*>(v.sphf + np);
-    v.lightf = reinterpret_cast<const DevSphereLightF*>(v.primf + np);
+    v.cone = reinterpret_cast<const DevSphereCone*>(v.primf + np);
+    v.lightf = reinterpret_cast<const DevSphereLightF*>(v.cone + np);
     v.mesh = reinterpret_cast<const DevMesh*>(v.lightf + (size_t)nl * np);
     v.nm = g->n_meshes;
     v.tri = reinterpret_cast<const DevTri*>(v.mesh + v.nm);
@@ -421,9 +423,34 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
 
 // Closest hit of a primary ray Line(eye, sp): deltaP and |deltaP|^2 per sphere were computed for this
 // eye by rt_prepare_kernel with the reference's operations (:740, :750).
+// One sphere of a primary ray: FP32 filter on the per-eye image, then the exact test (:747-772) and the
+// strict-< closest-hit update (:811-813).
+__device__ __forceinline__ void primary_sphere(const SceneView& V, const Ray& r, int k, double eps, int* kind,
+                                               double* best, d3* hp) {
+    const DevSpherePrimF& f = V.primf[k];
+    float uD = r.ux * f.dx;
+    uD = fmaf(r.uy, f.dy, uD);
+    uD = fmaf(r.uz, f.dz, uD);
+    if (fmaf(uD, uD, f.c0) < 0.0f) return;                  // certain disc < 0
+    const DevSpherePrim& pp = V.prim[k];
+    d3 q;
+    if (sphere_hit_dp(ld3(pp.dP), pp.dd, V.sph[k].r2, r.p0, r.u, eps, &q)) {
+        double dist = len_fast(sub(q, r.p0));
+        if (dist < *best || *best < 0.0) {
+            *best = dist;
+            *kind = 1 + k;
+            *hp = q;
+        }
+    }
+}
+
+// Closest hit of a primary ray Line(eye, sp): deltaP and |deltaP|^2 per sphere were computed for this
+// eye by rt_prepare_kernel with the reference's operations (:740, :750).  `cone` (np >= kConeMin): bit k
+// set when sphere k < 64 may be hit by some ray of this wave (primary_cone_mask); the others are
+// provably missed and skipped.  Spheres are still visited in increasing k (tie order unchanged).
 template <bool FULL>
 __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray& r, d3 bdP, double bdd,
-                                                   d3* hp) {
+                                                   uint64_t cone, d3* hp) {
     const DevScene* S = V.S;
     if (!bound_pass_dp(S, bdP, bdd, r.u)) return -1;
     int kind = -1;
@@ -437,7 +464,12 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
         }
     }
     const double eps = S->eps;
-    for (int k0 = 0; k0 < V.np; k0 += kChunk) {
+    int k0 = 0;
+    if (V.np >= kConeMin) {
+        for (uint64_t m = cone; m; m &= m - 1) primary_sphere(V, r, __builtin_ctzll(m), eps, &kind, &best, hp);
+        k0 = 64;
+    }
+    for (; k0 < V.np; k0 += kChunk) {
         uint32_t pass = 0;
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
@@ -464,6 +496,41 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
     }
     if (FULL) meshes_closest(V, r, eps, &kind, &best, hp);
     return kind;
+}
+
+// chord(phi) = |x - y| for unit vectors at angle phi = asin(s): s sqrt(2 / (1 + sqrt(1 - s^2))).
+__device__ __host__ __forceinline__ float chord_of_sin(float s) {
+    return s * sqrtf(2.0f / (1.0f + sqrtf(fmaxf(0.0f, 1.0f - s * s))));
+}
+
+// Per-wave culling of primary rays (V.np >= kConeMin; all 64 lanes must be active).  The wave's rays go
+// from the eye through the screen points of its 8 x 8 block, all within R = 3.5 sqrt(2) pitch of the
+// block centre c, hence (exact geometry) within angle asin(R / |c - eye|) of a = unit(c - eye): chord
+// distance |u - a| <= rho.  A ray that hits sphere k has |u - v_k| <= chord_k (DevSphereCone, rounded
+// up, radius inflated for FP64 rounding), so |a - v_k| <= rho + chord_k + slack, where `slack` (host,
+// RenderParams) bounds the FP32 error of a and of the test itself.  Lane j evaluates sphere j; the
+// ballot is the mask of spheres this wave must test.  NaNs keep the sphere.
+__device__ __forceinline__ uint64_t primary_cone_mask(const SceneView& V, const float look[3],
+                                                      const float right[3], const float upp[3],
+                                                      const float eye[3], float pitch, float ci, float cj,
+                                                      float slack, int lane) {
+    const float a_r = pitch * ci, a_u = pitch * cj;
+    float dx = fmaf(a_u, upp[0], fmaf(a_r, right[0], look[0])) - eye[0];
+    float dy = fmaf(a_u, upp[1], fmaf(a_r, right[1], look[1])) - eye[1];
+    float dz = fmaf(a_u, upp[2], fmaf(a_r, right[2], look[2])) - eye[2];
+    const float dn = sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz)));
+    const float sn = (3.5f * 1.41422f * 1.001f) * pitch / dn;
+    if (!(sn < 0.5f)) return ~0ull;                         // eye too close to the screen: no culling
+    const float rho = chord_of_sin(sn) + slack;
+    dx /= dn, dy /= dn, dz /= dn;
+    bool keep = false;
+    if (lane < V.np) {
+        const DevSphereCone& c = V.cone[lane];
+        const float ex = dx - c.vx, ey = dy - c.vy, ez = dz - c.vz;
+        const float lim = rho + c.chord;
+        keep = !(fmaf(ex, ex, fmaf(ey, ey, ez * ez)) > lim * lim);
+    }
+    return __ballot(keep);
 }
 
 // Shadow test: intersects() of g_scene.intersection(Line(pt, Lpos)) (:1216-1221), any hit.
@@ -597,7 +664,8 @@ __device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 
 // the transmitted ray (transparency != 0 and |transparency| > eps), weighted by that vector (:1238-1247),
 // so the colour is the right-nested local[0] + w[0] % (local[1] + w[1] % (...)).  TRANSP = false: all
 // materials opaque, no meshes, w = (1,1,1) (multiplication by 1.0 is exact) and any-hit shadows.
-// PRIMARY: p0 is the camera and V.prim/V.primf hold its per-sphere data; (bdP, bdd) = bc - eye, |.|^2.
+// PRIMARY: p0 is the camera and V.prim/V.primf hold its per-sphere data; (bdP, bdd) = bc - eye, |.|^2;
+// cone = primary_cone_mask of the wave (used when np >= kConeMin).
 // seg / shadow count the rays actually traced.
 // The bounce loop is not unrolled and the per-level colours local[k] (and, TRANSP, the level's material
 // for w[k]) wait in LDS until the right-nested sum, not in registers: slot[(3k + c) kSlotStride],
@@ -605,8 +673,8 @@ __device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 
 constexpr int kSlotStride = 256;
 
 template <int B, bool PRIMARY, bool TRANSP>
-__device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, double bdd, uint32_t* seg,
-                                    uint32_t* shadow, double* slot, int* mslot) {
+__device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, double bdd, uint64_t cone,
+                                    uint32_t* seg, uint32_t* shadow, double* slot, int* mslot) {
     const DevScene* S = V.S;
     int levels = 0;
     Ray r;
@@ -623,7 +691,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
             d3 p;
             int kind;
             if (PRIMARY && lvl == 0) {
-                kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, &p);
+                kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p);
             } else {
                 set_origin_f32(S, &r);
                 kind = closest_hit<TRANSP>(V, r, &p);

@@ -392,7 +392,7 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     // inside or near a sphere (|C - L| <= r (1 + 2^-20) or |C - L| <= 2^-14 (1 + |L| + |C|)) gets c = -inf
     // (always tested), padding spheres c = +inf (never).
     rt::DevSphereLightF* lightf = reinterpret_cast<rt::DevSphereLightF*>(
-        reinterpret_cast<rt::DevSpherePrimF*>(sphf + np) + np);
+        reinterpret_cast<rt::DevSphereCone*>(reinterpret_cast<rt::DevSpherePrimF*>(sphf + np) + np) + np);
     for (int i = 0; i < s->n_lights; ++i) {
         const HP L = hp(s->lights[i].position);
         const double aL = std::max(std::fabs(L.x), std::max(std::fabs(L.y), std::fabs(L.z)));

@@ -18,6 +18,7 @@
 // :1184-1249, intersection code :611-823, :1084-1113).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -59,6 +60,8 @@ struct RenderParams {
     int32_t np;
     int32_t nl;
     int32_t wg_staging;                        // 1: stage the 32 x 8 tile in LDS behind a workgroup barrier
+    float look32[3], right32[3], upp32[3], eye32[3], pitch32;   // FP32 camera for primary_cone_mask
+    float cone_slack;                          // its error bound (render_params)
 };
 
 // Image row (within its frame) of local row lr; local rows are frame-major (rt_rows.frames).
@@ -120,6 +123,18 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
     const int lr = ty * kTileH + cy;
     const bool valid = i < P.width && lr < P.local_rows;
 
+    // Per-wave sphere culling (all lanes active here).  The block's rows must be contiguous image rows.
+    uint64_t cone = ~0ull;
+    if (P.np >= kConeMin) {
+        // Within one frame global_row_of is increasing, so jb - ja == 7 means 8 consecutive rows.
+        const int lr0 = ty * kTileH, ja = global_row_of(P, lr0), jb = global_row_of(P, lr0 + 7);
+        const bool one_frame = P.frames <= 1 || lr0 / P.frame_rows == (lr0 + 7) / P.frame_rows;
+        if (one_frame && jb - ja == 7)
+            cone = primary_cone_mask(V, P.look32, P.right32, P.upp32, P.eye32, P.pitch32,
+                                     (float)(tx * kTileW + wave * 8 + P.bottom_x) + 3.5f,
+                                     (float)(ja + P.bottom_y) + 3.5f, P.cone_slack, lane);
+    }
+
     d3 col = mk(0.0, 0.0, 0.0);
     uint32_t seg = 0, sh = 0;
     if (valid) {
@@ -129,7 +144,7 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
         d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(i + P.bottom_x), right)),
                     scl(P.pitch * (double)(j + P.bottom_y), upp));
         d3 bdP = sub(ld3(V.S->bc), eye);           // bounding-sphere deltaP for p0 = camera
-        col = trace<B, true, TRANSP>(V, eye, sp, bdP, dot(bdP, bdP), &seg, &sh, slot, mslot);
+        col = trace<B, true, TRANSP>(V, eye, sp, bdP, dot(bdP, bdP), cone, &seg, &sh, slot, mslot);
     }
 
     if (!P.wg_staging) {
@@ -178,6 +193,7 @@ __global__ __launch_bounds__(kThreads) void rt_prepare_kernel(DevScene* __restri
     DevSpherePrim* prim = reinterpret_cast<DevSpherePrim*>(sph + np);
     DevSphereF* sphf = reinterpret_cast<DevSphereF*>(prim + np);
     DevSpherePrimF* primf = reinterpret_cast<DevSpherePrimF*>(sphf + np);
+    DevSphereCone* cone = reinterpret_cast<DevSphereCone*>(primf + np);
     const d3 eye = mk(ex, ey, ez);
     const int k = blockIdx.x * kThreads + threadIdx.x;
     if (k == 0) { g->eye[0] = ex; g->eye[1] = ey; g->eye[2] = ez; }
@@ -195,6 +211,26 @@ __global__ __launch_bounds__(kThreads) void rt_prepare_kernel(DevScene* __restri
     f.dx = (float)dP.x; f.dy = (float)dP.y; f.dz = (float)dP.z;
     f.c0 = __double2float_ru(c0);
     primf[k] = f;
+    // Cone of directions from the eye that can hit sphere k (primary_cone_mask).  r' covers the FP64
+    // test's rounding (disc error < 4 ulp of 3 D^2 < D^2 2^-48): r'^2 = r2 (1 + 2^-20) + D^2 2^-46.
+    DevSphereCone cn;
+    if (!(r2 >= 0.0)) {                                     // padding: never kept
+        cn.vx = cn.vy = cn.vz = 1e30f;
+        cn.chord = 0.0f;
+    } else {
+        double D = sqrt(dd);
+        double rp = sqrt(r2 * (1.0 + 0x1p-20) + dd * 0x1p-46);
+        double sn = rp / D;
+        if (!(sn < 0.999)) {                                // eye inside / at the sphere: always kept
+            cn.vx = cn.vy = cn.vz = 0.0f;
+            cn.chord = 4.0f;
+        } else {
+            double ch = sn * sqrt(2.0 / (1.0 + sqrt(1.0 - sn * sn))) + 0x1p-20;
+            cn.vx = (float)(dP.x / D); cn.vy = (float)(dP.y / D); cn.vz = (float)(dP.z / D);
+            cn.chord = __double2float_ru(ch);
+        }
+    }
+    cone[k] = cn;
 }
 
 template <int B, bool TRANSP>
@@ -210,8 +246,8 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
     const SceneView V = view_of(S, S, S->n_padded, S->n_lights);
     double* slot = reinterpret_cast<double*>(smem) + threadIdx.x;
     int* mslot = reinterpret_cast<int*>(smem + 3 * 8 * (B + 1) * kSlotStride) + threadIdx.x;
-    d3 c = trace<B, false, TRANSP>(V, ld3(starts + 3 * k), ld3(ends + 3 * k), mk(0.0, 0.0, 0.0), 0.0, &seg, &sh,
-                                   slot, mslot);
+    d3 c = trace<B, false, TRANSP>(V, ld3(starts + 3 * k), ld3(ends + 3 * k), mk(0.0, 0.0, 0.0), 0.0, ~0ull, &seg,
+                                   &sh, slot, mslot);
     if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
     if (rc) rc[k] = seg | (sh << 16);
 }
@@ -456,6 +492,22 @@ static int render_params(const rt_ctx* c, const rt_camera* cam, int W, int H, in
     P->np = c->n_padded;
     P->nl = c->n_lights;
     P->wg_staging = c->wg_staging;
+    // FP32 camera for the per-wave cone culling, and the bound on its error as a chord distance: every
+    // FP32 coordinate is below M in magnitude and carries < 16 roundings, and |sp - eye| >= |look - eye|
+    // (right, up' are orthogonal to look - eye), so direction errors are < 64 eps32 M / |look - eye|.
+    double M = 1.0, D2 = 0.0;
+    for (int q = 0; q < 3; ++q) {
+        P->look32[q] = (float)P->look[q];
+        P->right32[q] = (float)P->right[q];
+        P->upp32[q] = (float)P->upp[q];
+        P->eye32[q] = (float)P->eye[q];
+        M = std::max(M, std::fabs(P->look[q]) + std::fabs(P->eye[q]));
+        D2 += (P->look[q] - P->eye[q]) * (P->look[q] - P->eye[q]);
+    }
+    P->pitch32 = (float)P->pitch;
+    M += std::fabs(P->pitch) * (std::abs((double)P->bottom_x) + std::abs((double)P->bottom_y) + W + H + 16.0);
+    const double slack = 0x1p-16 + 64.0 * 0x1p-24 * M / std::sqrt(D2);
+    P->cone_slack = (D2 > 0.0 && slack < 0.25) ? (float)slack : 8.0f;   // 8: keep every sphere
     return RT_OK;
 }
 

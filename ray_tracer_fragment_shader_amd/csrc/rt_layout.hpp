@@ -6,12 +6,14 @@
 //   DevSpherePrim[np]   primary-ray FP64 data (per eye)  ┘ (lds_bytes)
 //   DevSphereF[np]      FP32 filter image               ┐ read through the scalar cache (SGPR operands),
 //   DevSpherePrimF[np]  primary-ray FP32 filter (per eye)│ one batch of kChunk records per s_load group
+//   DevSphereCone[np]   primary-ray cone of each sphere (per eye): per-wave culling
 //   DevSphereLightF[nl][np]  shadow-ray FP32 cone filter ┘ per light (line through the light)
 //   DevMesh[nm]         tetrahedra / cubes: bounding sphere, triangle range, material, child index
 //   DevTri[nt]          their triangles (world vertex 0, u, v, n, uv, uu, vv, den)
 // np = n_spheres rounded up to kChunk; the padding spheres have r2 = -inf and filter terms = -inf, so
-// they are rejected by the filter and can never hit.  The two *Prim arrays depend on the camera eye and
-// are (re)written on the device by rt_prepare_kernel whenever rt_render_dev sees a new eye.
+// they are rejected by the filter and can never hit.  The two *Prim arrays and DevSphereCone depend on
+// the camera eye and are (re)written on the device by rt_prepare_kernel whenever rt_render_dev sees a
+// new eye.
 #pragma once
 
 #include <stdint.h>
@@ -19,6 +21,7 @@
 namespace rt {
 
 constexpr int kChunk = 4;              // spheres per branch-free filter batch
+constexpr int kConeMin = 16;           // per-wave cone culling of primary rays from this many (padded) spheres
 
 // FP32 filter margin factor: 256 unit roundoffs of binary32.  The filter's own error is below
 // 64 * 2^-24 * (S^2 + r^2) (error budget in rt_device.hpp, sphere_reject32), so a margin of
@@ -76,6 +79,10 @@ struct alignas(16) DevSpherePrimF {    // FP32 filter for primary rays: f32(dP),
     float dx, dy, dz, c0;
 };
 
+struct alignas(16) DevSphereCone {     // primary rays: f32(unit(C - eye)) and the chord radius of the
+    float vx, vy, vz, chord;           // sphere's cone of directions seen from the eye (rounded up)
+};
+
 struct alignas(16) DevSphereLightF {   // shadow rays to light i: f32(unit(C - L)) and cos(phi) - margin,
     float vx, vy, vz, c;               // phi = asin(r / |C - L|); c = -inf: always test, +inf: never (padding)
 };
@@ -113,7 +120,8 @@ inline constexpr int lds_bytes_for(int n) {
 
 inline constexpr int scene_bytes_for(int n, int n_meshes = 0, int n_tris = 0, int n_lights = 0) {
     return lds_bytes_for(n) +
-           (int)((sizeof(DevSphereF) + sizeof(DevSpherePrimF) + sizeof(DevSphereLightF) * (unsigned)n_lights) *
+           (int)((sizeof(DevSphereF) + sizeof(DevSpherePrimF) + sizeof(DevSphereCone) +
+                  sizeof(DevSphereLightF) * (unsigned)n_lights) *
                  (unsigned)padded_spheres(n)) +
            (int)(sizeof(DevMesh) * (unsigned)n_meshes + sizeof(DevTri) * (unsigned)n_tris);
 }

@@ -396,3 +396,38 @@ def test_math_fast_paths(tr):
     assert _same_bits(o[:, 8], o[:, 3]).all()
     fast = (s >= 2.0 ** -700) & (s <= 2.0 ** 700)
     assert fast.sum() > n // 2 and (~fast).sum() > 100        # both paths exercised
+
+
+@pytest.mark.parametrize("G,hb,frames", [(1, 8, 1), (3, 5, 2), (2, 3, 3)])
+def test_primary_cone_culling_bands_frames(tr, G, hb, frames):
+    """64 spheres (>= kConeMin: per-wave primary culling) under row bands and stacked frames, where a
+    wave's 8 rows may straddle bands or frames."""
+    cfg = scenes.CONFIGS["c5"]
+    W, H = 203, 97
+    cam = cfg.camera(W, H)
+    for r in range(G):
+        rows = scenes.rows(hb, G, r, frames)
+        got, rc = _render64(tr, cfg.scene(), cam, W, H, 2, rows=rows)
+        want, want_rc = po.render(cfg.scene().to_abi(), cam, W, H, 2, rows=rows)
+        _assert_parity(got, want)
+        assert np.array_equal(rc, want_rc)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_primary_cone_culling_random_cameras(tr, seed):
+    """Many spheres seen from random eyes (close up, inside a sphere, far away) and pitches."""
+    rng = np.random.default_rng(300 + seed)
+    sc = _random_scene(rng, int(rng.integers(16, 120)), int(rng.integers(1, 3)))
+    W, H = 120, 88
+    cam = scenes.make_camera(W, H, float(rng.choice([0.05, 0.5, 2.0, 9.0])))
+    if seed % 3 == 1:                                 # eye among (possibly inside) the spheres
+        sp = sc.spheres[int(rng.integers(0, len(sc.spheres)))]
+        c = np.array(sp.center()) + np.array([0.0, 0.0, -160.0])
+        eye = c + rng.normal(size=3) * sp.radius * float(rng.choice([0.5, 1.5]))
+        cam.eye = abi.vec3(eye)
+    elif seed % 3 == 2:                               # far away
+        cam.eye = abi.vec3((0.0, 3000.0, 9000.0))
+    got, rc = _render64(tr, sc, cam, W, H, 1)
+    want, want_rc = po.render(sc.to_abi(), cam, W, H, 1)
+    _assert_parity(got, want)
+    assert np.array_equal(rc, want_rc)
