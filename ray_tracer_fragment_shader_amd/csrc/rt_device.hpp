@@ -376,6 +376,9 @@ __device__ __forceinline__ bool sphere_hit(const DevSphere& sp, d3 p0, d3 u, dou
     return sphere_hit_dp(dP, dot(dP, dP), sp.r2, p0, u, eps, p);
 }
 
+// Bits of the spheres a 64-bit mask may name: k < min(np, 64).
+__device__ __forceinline__ uint64_t sphere_bits(int np) { return np >= 64 ? ~0ull : ((1ull << np) - 1); }
+
 // Closest hit of g_scene (:796-821): Euclidean distance |p - p0|, strict <, board (child 0) first.
 // kind: -1 miss, 0 board, 1 + k sphere k.
 // Spheres go in batches of kChunk: the FP32 filter of the whole batch is evaluated branch-free (records
@@ -401,8 +404,10 @@ __device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const R
     }
 }
 
-template <bool FULL>
-__device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3* hp) {
+// `mask` (np >= kConeMin): spheres k < 64 this wave's rays may hit (ray_bundle_mask); the rest of the
+// first 64 are skipped.  Spheres are visited in increasing k either way.
+template <bool FULL, bool CULL = false>
+__device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3* hp, uint64_t mask = ~0ull) {
     const DevScene* S = V.S;
     if (!bound_pass(S, r.p0, r.u)) return -1;
     int kind = -1;
@@ -416,7 +421,24 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
         }
     }
     const double eps = S->eps;
-    for (int k0 = 0; k0 < V.np; k0 += kChunk) sphere_batch_closest(V, r, k0, eps, &kind, &best, hp);
+    int k0 = 0;
+    if (CULL && V.np >= kConeMin) {
+        for (uint64_t m = mask & sphere_bits(V.np); m; m &= m - 1) {
+            const int k = __builtin_ctzll(m);
+            if (sphere_reject32(V.sphf[k], r)) continue;
+            d3 q;
+            if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) {
+                double dist = len_fast(sub(q, r.p0));       // :811-812
+                if (dist < best || best < 0.0) {            // :813
+                    best = dist;
+                    kind = 1 + k;
+                    *hp = q;
+                }
+            }
+        }
+        k0 = 64;
+    }
+    for (; k0 < V.np; k0 += kChunk) sphere_batch_closest(V, r, k0, eps, &kind, &best, hp);
     if (FULL) meshes_closest(V, r, eps, &kind, &best, hp);
     return kind;
 }
@@ -466,7 +488,8 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
     const double eps = S->eps;
     int k0 = 0;
     if (V.np >= kConeMin) {
-        for (uint64_t m = cone; m; m &= m - 1) primary_sphere(V, r, __builtin_ctzll(m), eps, &kind, &best, hp);
+        for (uint64_t m = cone & sphere_bits(V.np); m; m &= m - 1)
+            primary_sphere(V, r, __builtin_ctzll(m), eps, &kind, &best, hp);
         k0 = 64;
     }
     for (; k0 < V.np; k0 += kChunk) {
@@ -533,6 +556,111 @@ __device__ __forceinline__ uint64_t primary_cone_mask(const SceneView& V, const 
     return __ballot(keep);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Wave-level culling of secondary and shadow rays (np >= kConeMin).  Called with all 64 lanes active;
+// `on` marks the lanes whose ray the mask must cover.  Lane j evaluates sphere j (< 64) against the
+// wave's bundle; the ballot is the mask of spheres to test.  Lanes whose ray has a non-finite
+// coordinate widen the bundle to everything (the reference reports NaN rays as hits).
+
+// max over the 64 lanes (DPP: quad permutes, row mirrors, row broadcasts; GFX9 encodings).
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROWS, 0xF, false));
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+    v = fmaxf(v, dpp_f32<0xB1>(v));                          // quad_perm [1,0,3,2]
+    v = fmaxf(v, dpp_f32<0x4E>(v));                          // quad_perm [2,3,0,1]
+    v = fmaxf(v, dpp_f32<0x141>(v));                         // row_half_mirror
+    v = fmaxf(v, dpp_f32<0x140>(v));                         // row_mirror
+    v = fmaxf(v, dpp_f32<0x142, 0xA>(v));                    // row_bcast:15 -> rows 1, 3
+    v = fmaxf(v, dpp_f32<0x143, 0xC>(v));                    // row_bcast:31 -> rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+__device__ __forceinline__ float lane_f32(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+__device__ __forceinline__ float inf_if_nan(float v) { return v >= 0.0f ? v : __builtin_inff(); }
+
+// Reflected / transmitted rays (p_l, u_l): o, a = origin and direction of the first `on` lane,
+// rho_o >= |p_l - o|, rho_d >= |u_l - a| (chord).  A ray that hits sphere k (exact FP64 test) passes
+// within r' of C_k (r'^2 = r^2 (1 + 2^-20) + D^2 2^-46 covers the test's rounding), so the ray from o
+// with the same direction passes within R = r' + rho_o: either |C_k - o| <= R, or the angle between u_l
+// and v = unit(C_k - o) is at most asin(R / |C_k - o|), i.e. |a - v| <= rho_d + chord(R / |C_k - o|).
+// FP32 coordinates carry < 2^-20 relative error; R gets 2^-12 (|o| + |C| + 1) absolute and the chord
+// test 2^-14 of slack.
+__device__ __forceinline__ uint64_t ray_bundle_mask(const SceneView& V, bool on, const Ray& r) {
+    const int lane = __lane_id();
+    const uint64_t onm = __ballot(on);
+    if (!onm) return 0;
+    const int f = __builtin_ctzll(onm);
+    const float ox = lane_f32(r.px, f), oy = lane_f32(r.py, f), oz = lane_f32(r.pz, f);
+    const float ax = lane_f32(r.ux, f), ay = lane_f32(r.uy, f), az = lane_f32(r.uz, f);
+    float dp = 0.0f, du = 0.0f;
+    if (on) {
+        const float px = r.px - ox, py = r.py - oy, pz = r.pz - oz;
+        const float ux = r.ux - ax, uy = r.uy - ay, uz = r.uz - az;
+        dp = inf_if_nan(sqrtf(fmaf(px, px, fmaf(py, py, pz * pz))));
+        du = inf_if_nan(sqrtf(fmaf(ux, ux, fmaf(uy, uy, uz * uz))));
+    }
+    const float rho_o = wave_max(dp), rho_d = wave_max(du);
+    if (!(rho_d < 1.0f) || !(rho_o < 1e30f)) return ~0ull;   // spread too wide: no culling
+    bool keep = false;
+    if (lane < V.np) {
+        const DevSphereF& c = V.sphf[lane];
+        if (c.rm >= 0.0f) {                                   // padding spheres: rm = -inf
+            const float vx = c.cx - ox, vy = c.cy - oy, vz = c.cz - oz;
+            const float D = sqrtf(fmaf(vx, vx, fmaf(vy, vy, vz * vz)));
+            const float Dm = D + rho_o;
+            const float scale = fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz))) +
+                                fmaxf(fabsf(c.cx), fmaxf(fabsf(c.cy), fabsf(c.cz))) + 1.0f;
+            const float R = (sqrtf(fmaf(c.rm, 1.0f + 0x1p-20f, Dm * Dm * 0x1p-46f)) + rho_o) * (1.0f + 0x1p-12f) +
+                            0x1p-12f * scale;
+            if (!(D > R)) {
+                keep = true;
+            } else {
+                const float lim = rho_d + chord_of_sin(R / D) + 0x1p-14f;
+                const float ex = ax - vx / D, ey = ay - vy / D, ez = az - vz / D;
+                keep = !(fmaf(ex, ex, fmaf(ey, ey, ez * ez)) > lim * lim);
+            }
+        }
+    }
+    return __ballot(keep);
+}
+
+// Shadow rays to light li: every ray lies on a line through the light, with direction w_l = u_l.
+// a = w of the first `on` lane, rho >= |w_l - a|.  The light record gives v_k and c_k <= cos(phi_k),
+// so a line through L that meets sphere k has |w -+ v_k| <= chord_k = sqrt(2 - 2 c_k) for one sign, and
+// then |a -+ v_k| <= rho + chord_k (+ 2^-14 for FP32).  c_k = -inf: always kept; +inf (padding): never.
+__device__ __forceinline__ uint64_t shadow_bundle_mask(const SceneView& V, bool on, const Ray& r, int li) {
+    const int lane = __lane_id();
+    const uint64_t onm = __ballot(on);
+    if (!onm) return 0;
+    const int f = __builtin_ctzll(onm);
+    const float ax = lane_f32(r.ux, f), ay = lane_f32(r.uy, f), az = lane_f32(r.uz, f);
+    float du = 0.0f;
+    if (on) {
+        const float ux = r.ux - ax, uy = r.uy - ay, uz = r.uz - az;
+        du = inf_if_nan(sqrtf(fmaf(ux, ux, fmaf(uy, uy, uz * uz))));
+    }
+    const float rho = wave_max(du);
+    if (!(rho < 1.0f)) return ~0ull;
+    bool keep = false;
+    if (lane < V.np) {
+        const DevSphereLightF& c = V.lightf[li * V.np + lane];
+        if (c.c <= 1.0f) {
+            const float lim = rho + sqrtf(fmaxf(0.0f, 2.0f - 2.0f * c.c)) + 0x1p-14f;
+            const float l2 = lim * lim;
+            const float ex = ax - c.vx, ey = ay - c.vy, ez = az - c.vz;
+            const float fx = ax + c.vx, fy = ay + c.vy, fz = az + c.vz;
+            keep = !(fmaf(ex, ex, fmaf(ey, ey, ez * ez)) > l2) || !(fmaf(fx, fx, fmaf(fy, fy, fz * fz)) > l2);
+        }
+    }
+    return __ballot(keep);
+}
+
 // Shadow test: intersects() of g_scene.intersection(Line(pt, Lpos)) (:1216-1221), any hit.
 // Spheres are filtered with the light's cone records: the ray lies on a line through light `li`, which
 // meets sphere k only if |u . v_k| >= cos(phi_k) (host builder, rt_host.cpp).  FP32 error of the lane's
@@ -540,13 +668,27 @@ __device__ __forceinline__ uint64_t primary_cone_mask(const SceneView& V, const 
 // far inside the 2^-16 folded into c_k; the FP64 hit test's own rounding moves the line by ~1e-13
 // relative, likewise covered.  A NaN direction is not rejected (it compares false), as the FP64 test
 // reports NaN rays as hits.
-template <bool FULL>
-__device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li) {
+template <bool FULL, bool CULL = false>
+__device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull) {
     const DevScene* S = V.S;
     if (!bound_pass(S, r.p0, r.u)) return false;
     const double eps = S->eps;
     const DevSphereLightF* lf = V.lightf + li * V.np;
-    for (int k0 = 0; k0 < V.np; k0 += kChunk) {
+    int k0 = 0;
+    if (CULL && V.np >= kConeMin) {                               // mask: shadow_bundle_mask
+        for (uint64_t m = mask & sphere_bits(V.np); m; m &= m - 1) {
+            const int k = __builtin_ctzll(m);
+            const DevSphereLightF& f = lf[k];
+            float t = r.ux * f.vx;
+            t = fmaf(r.uy, f.vy, t);
+            t = fmaf(r.uz, f.vz, t);
+            if (fabsf(t) < f.c) continue;
+            d3 q;
+            if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) return true;
+        }
+        k0 = 64;
+    }
+    for (; k0 < V.np; k0 += kChunk) {
         uint32_t pass = 0;
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
@@ -631,10 +773,11 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
 }
 
 // Local illumination of one hit over all lights (:1213-1228).  u = incoming ray direction,
-// rdir = reflectedRay().direction().
+// rdir = reflectedRay().direction().  `hit` marks the lanes whose colour is wanted.  CULL: called by all
+// lanes of the wave, the light loop stays converged for shadow_bundle_mask; otherwise only by hit lanes.
 // FULL: meshes may be present and materials may be transparent (closest-hit shadows, :1219-1221).
-template <bool FULL>
-__device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 u, d3 rdir) {
+template <bool FULL, bool CULL>
+__device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, int mat, d3 u, d3 rdir) {
     const DevScene* S = V.S;
     const DevMat& M = S->mat[mat];
     d3 amb = ld3(M.amb), dif = ld3(M.diff), spc = ld3(M.spec);
@@ -649,7 +792,11 @@ __device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 
         double dl;                                          // shadowRay.length()
         d3 sdir = unit(sd, &dl);                            // shadowRay.direction()
         set_dir(&sr, sd, sdir);
-        if (!(FULL ? occluded_transparent(V, sr) : occluded<false>(V, sr, i))) {
+        uint64_t m = ~0ull;
+        if (CULL && !FULL && V.np >= kConeMin) m = shadow_bundle_mask(V, hit, sr, i);
+        bool lit = false;
+        if (hit) lit = !(FULL ? occluded_transparent(V, sr) : occluded<false, CULL>(V, sr, i, m));
+        if (lit) {
             double a = S->att / (S->att + dl * dl);         // attenuation (:1181)
             d3 lC = scl(a, ld3(S->light[i].col));           // :1223
             d3 term = add(add(had(amb, lC), scl(fabs(dot(n, sdir)), had(dif, lC))), scl(ks, had(spc, lC)));
@@ -667,12 +814,37 @@ __device__ __forceinline__ d3 shade(const SceneView& V, d3 p, d3 n, int mat, d3 
 // PRIMARY: p0 is the camera and V.prim/V.primf hold its per-sphere data; (bdP, bdd) = bc - eye, |.|^2;
 // cone = primary_cone_mask of the wave (used when np >= kConeMin).
 // seg / shadow count the rays actually traced.
-// The bounce loop is not unrolled and the per-level colours local[k] (and, TRANSP, the level's material
-// for w[k]) wait in LDS until the right-nested sum, not in registers: slot[(3k + c) kSlotStride],
+// CULL (>= kConeMin spheres): called by all 64 lanes of a wave, the culling masks reduce over it.
+// The per-level colours
+// local[k] (and, TRANSP, the level's material for w[k]) wait in LDS until the right-nested sum, not in registers: slot[(3k + c) kSlotStride],
 // mslot[k kSlotStride], component-major so a wave's 64 lanes touch 64 consecutive words.
 constexpr int kSlotStride = 256;
 
-template <int B, bool PRIMARY, bool TRANSP>
+// A hit at level lvl: park its colour in LDS and turn r into the continuation ray (:1238-1247).
+template <int B, bool TRANSP>
+__device__ __forceinline__ void continue_ray(const SceneView& V, int lvl, int kind, int mat, d3 p, d3 n, d3 rd,
+                                             d3 rdir, d3 c, Ray* r, int* levels, uint32_t* nsh, double* slot,
+                                             int* mslot) {
+    const DevScene* S = V.S;
+    double* sl = slot + 3 * lvl * kSlotStride;
+    sl[0] = c.x;
+    sl[kSlotStride] = c.y;
+    sl[2 * kSlotStride] = c.z;
+    *nsh += V.nl;
+    *levels = lvl + 1;
+    if (TRANSP && S->mat[mat].transmit) {
+        d3 pt = transmitted_end(V, kind, mat, p, r->u, n);
+        d3 td = sub(pt, p);                                 // transmittedRay = Line(p, p + t)
+        r->p0 = p;                                          // the next level traces the continuation
+        set_dir(r, td, unit(td));
+    } else {
+        r->p0 = p;
+        set_dir(r, rd, rdir);
+    }
+    if (TRANSP) mslot[lvl * kSlotStride] = mat;
+}
+
+template <int B, bool PRIMARY, bool TRANSP, bool CULL>
 __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, double bdd, uint64_t cone,
                                     uint32_t* seg, uint32_t* shadow, double* slot, int* mslot) {
     const DevScene* S = V.S;
@@ -684,13 +856,40 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
     uint32_t nseg = 0, nsh = 0;
 #pragma unroll
     for (int lvl = 0; lvl <= B; ++lvl) {
-        bool alive = lvl == 0 || levels == lvl;
+        const bool alive = lvl == 0 || levels == lvl;
         if (!__any(alive)) break;                           // the whole wave has missed: early out
-        if (alive) {
+        const bool first = PRIMARY && lvl == 0;
+        if (CULL) {
+            // All lanes stay in the level body: ray_bundle_mask and shade's shadow_bundle_mask reduce over
+            // the wave.
+            uint64_t smask = ~0ull;
+            if (!first) {
+                set_origin_f32(S, &r);
+                if (V.np >= kConeMin) smask = ray_bundle_mask(V, alive, r);
+            }
+            d3 p = mk(0.0, 0.0, 0.0);
+            int kind = -1;
+            if (alive) {
+                ++nseg;
+                kind = first ? closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p)
+                             : closest_hit<TRANSP, true>(V, r, &p, smask);
+            }
+            const bool hit = kind >= 0;
+            if (!__any(hit)) break;
+            d3 n = mk(0.0, 0.0, 0.0), pe = n, rd = n, rdir = n;
+            int mat = 0;
+            if (hit) {
+                surface(V, kind, p, r.u, &n, &mat, &pe);
+                rd = sub(pe, p);                            // reflectedRay = Line(p, p + r)
+                rdir = unit(rd);                            // reflectedRay.direction()
+            }
+            const d3 c = shade<TRANSP, true>(V, hit, p, n, mat, r.u, rdir);
+            if (hit) continue_ray<B, TRANSP>(V, lvl, kind, mat, p, n, rd, rdir, c, &r, &levels, &nsh, slot, mslot);
+        } else if (alive) {
             ++nseg;
             d3 p;
             int kind;
-            if (PRIMARY && lvl == 0) {
+            if (first) {
                 kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p);
             } else {
                 set_origin_f32(S, &r);
@@ -702,22 +901,8 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                 surface(V, kind, p, r.u, &n, &mat, &pe);
                 d3 rd = sub(pe, p);                         // reflectedRay = Line(p, p + r)
                 d3 rdir = unit(rd);                         // reflectedRay.direction()
-                d3 c = shade<TRANSP>(V, p, n, mat, r.u, rdir);
-                double* sl = slot + 3 * lvl * kSlotStride;
-                sl[0] = c.x;
-                sl[kSlotStride] = c.y;
-                sl[2 * kSlotStride] = c.z;
-                nsh += V.nl;
-                levels = lvl + 1;
-                r.p0 = p;                                   // the next level traces the continuation
-                if (TRANSP && S->mat[mat].transmit) {
-                    d3 pt = transmitted_end(V, kind, mat, p, r.u, n);
-                    d3 td = sub(pt, p);                     // transmittedRay = Line(p, p + t)
-                    set_dir(&r, td, unit(td));
-                } else {
-                    set_dir(&r, rd, rdir);
-                }
-                if (TRANSP) mslot[lvl * kSlotStride] = mat;
+                const d3 c = shade<TRANSP, false>(V, true, p, n, mat, r.u, rdir);
+                continue_ray<B, TRANSP>(V, lvl, kind, mat, p, n, rd, rdir, c, &r, &levels, &nsh, slot, mslot);
             }
         }
     }

@@ -1,7 +1,8 @@
 // rt_kernel.hip — MI355X (gfx950) kernels and the device half of the C ABI (include/rt_api.h).
 //
 // Kernels
-//   rt_render_kernel<B, LDS>  one work-item per pixel, FP64, iterative bounce loop (rt_device.hpp).
+//   rt_render_kernel<B, LDS, MINW, TRANSP, CULL>  one work-item per pixel, FP64, iterative bounce loop
+//                             (rt_device.hpp); CULL: wave-level sphere culling for >= kConeMin spheres.
 //                             Workgroup = 256 work-items = 4 wave64; the workgroup owns a 32 x 8 pixel
 //                             tile and each wave an 8 x 8 sub-tile (square sub-tiles keep a wave's rays
 //                             coherent, so the __any early-out in the bounce loop fires for whole waves).
@@ -84,7 +85,7 @@ __device__ __forceinline__ unsigned char to_u8(double c) {
     return (unsigned char)(int)floor(v * 255.0 + 0.5);
 }
 
-template <int B, int LDS, int MINW, bool TRANSP>
+template <int B, int LDS, int MINW, bool TRANSP, bool CULL>
 __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
                                                              RenderParams P, float4* __restrict__ out32,
                                                              uchar4* __restrict__ out8,
@@ -135,17 +136,17 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
                                      (float)(ja + P.bottom_y) + 3.5f, P.cone_slack, lane);
     }
 
-    d3 col = mk(0.0, 0.0, 0.0);
+    // Every lane traces (trace() reduces over the wave): lanes outside the frame trace a clamped pixel
+    // and store nothing.
     uint32_t seg = 0, sh = 0;
-    if (valid) {
-        const int j = global_row_of(P, lr);
-        d3 right = ld3(P.right), upp = ld3(P.upp);
-        // Primary ray Line(camera, sp), SURVEY.md Appendix B (basis: rayTraceScreen :1270-1279).
-        d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(i + P.bottom_x), right)),
-                    scl(P.pitch * (double)(j + P.bottom_y), upp));
-        d3 bdP = sub(ld3(V.S->bc), eye);           // bounding-sphere deltaP for p0 = camera
-        col = trace<B, true, TRANSP>(V, eye, sp, bdP, dot(bdP, bdP), cone, &seg, &sh, slot, mslot);
-    }
+    const int ic = i < P.width ? i : P.width - 1, lrc = lr < P.local_rows ? lr : P.local_rows - 1;
+    const int j = global_row_of(P, lrc);
+    const d3 right = ld3(P.right), upp = ld3(P.upp);
+    // Primary ray Line(camera, sp), SURVEY.md Appendix B (basis: rayTraceScreen :1270-1279).
+    const d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(ic + P.bottom_x), right)),
+                      scl(P.pitch * (double)(j + P.bottom_y), upp));
+    const d3 bdP = sub(ld3(V.S->bc), eye);                  // bounding-sphere deltaP for p0 = camera
+    const d3 col = trace<B, true, TRANSP, CULL>(V, eye, sp, bdP, dot(bdP, bdP), cone, &seg, &sh, slot, mslot);
 
     if (!P.wg_staging) {
         // Direct stores: each wave writes its 8 x 8 block as 8 row segments (128 B of RGBA32F each) and
@@ -240,14 +241,15 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
                                                                  double* __restrict__ rgb,
                                                                  uint32_t* __restrict__ rc) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int k = blockIdx.x * kThreads + threadIdx.x;
-    if (k >= n) return;
+    // Every lane traces (trace() reduces over the wave); lanes past n repeat ray n - 1 and store nothing.
+    const int k = blockIdx.x * kThreads + threadIdx.x, kk = k < n ? k : n - 1;
     uint32_t seg = 0, sh = 0;
     const SceneView V = view_of(S, S, S->n_padded, S->n_lights);
     double* slot = reinterpret_cast<double*>(smem) + threadIdx.x;
     int* mslot = reinterpret_cast<int*>(smem + 3 * 8 * (B + 1) * kSlotStride) + threadIdx.x;
-    d3 c = trace<B, false, TRANSP>(V, ld3(starts + 3 * k), ld3(ends + 3 * k), mk(0.0, 0.0, 0.0), 0.0, ~0ull, &seg,
-                                   &sh, slot, mslot);
+    d3 c = trace<B, false, TRANSP, false>(V, ld3(starts + 3 * kk), ld3(ends + 3 * kk), mk(0.0, 0.0, 0.0), 0.0, ~0ull,
+                                   &seg, &sh, slot, mslot);
+    if (k >= n) return;
     if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
     if (rc) rc[k] = seg | (sh << 16);
 }
@@ -321,17 +323,17 @@ __global__ __launch_bounds__(kThreads) void rt_probe_math_kernel(int op, const d
 
 // ------------------------------------------------------------------------------------------------
 // Template dispatch.
-template <int LDS, int MINW, bool TRANSP>
+template <int LDS, int MINW, bool TRANSP, bool CULL = false>
 hipError_t launch_render_lds(int depth, dim3 grid, size_t lds, hipStream_t st, const DevScene* s,
                              const RenderParams& P, float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
 #define RT_CASE(b)                                                                                      \
     case b:                                                                                             \
         if (lds > 65536) {                                                                              \
-            hipError_t e_ = hipFuncSetAttribute((const void*)rt_render_kernel<b, LDS, MINW, TRANSP>,                  \
+            hipError_t e_ = hipFuncSetAttribute((const void*)rt_render_kernel<b, LDS, MINW, TRANSP, CULL>,                  \
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);  \
             if (e_ != hipSuccess) return e_;                                                            \
         }                                                                                               \
-        hipLaunchKernelGGL((rt_render_kernel<b, LDS, MINW, TRANSP>), grid, dim3(kThreads), lds, st, s, P, o32, o8,    \
+        hipLaunchKernelGGL((rt_render_kernel<b, LDS, MINW, TRANSP, CULL>), grid, dim3(kThreads), lds, st, s, P, o32, o8,    \
                            o64, orc);                                                                   \
         break;
     switch (depth) {
@@ -543,10 +545,14 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
         e = launch_render_lds<1, 1, false>(depth, grid, c->lds_bytes + stage, st, c->d_scene, P,
                                  reinterpret_cast<float4*>(rgba32f), reinterpret_cast<uchar4*>(rgba8), rgb64f,
                                  raycount);
-    else
-        e = (c->min_waves >= 5 && depth <= 3 ? launch_render_lds<0, 5, false> : launch_render_lds<0, 1, false>)(
-                depth, grid, stage, st, c->d_scene, P, reinterpret_cast<float4*>(rgba32f),
-                                 reinterpret_cast<uchar4*>(rgba8), rgb64f, raycount);
+    else {
+        // >= kConeMin spheres: the wave-culling variant (secondary and shadow rays, rt_device.hpp CULL).
+        const bool cull = c->n_padded >= kConeMin, mw5 = c->min_waves >= 5 && depth <= 3;
+        auto launch = cull ? (mw5 ? launch_render_lds<0, 5, false, true> : launch_render_lds<0, 1, false, true>)
+                           : (mw5 ? launch_render_lds<0, 5, false, false> : launch_render_lds<0, 1, false, false>);
+        e = launch(depth, grid, stage, st, c->d_scene, P, reinterpret_cast<float4*>(rgba32f),
+                   reinterpret_cast<uchar4*>(rgba8), rgb64f, raycount);
+    }
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_kernel launch: ") + hipGetErrorString(e));
     return RT_OK;
 }
