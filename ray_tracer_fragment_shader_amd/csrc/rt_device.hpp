@@ -527,8 +527,8 @@ __device__ __host__ __forceinline__ float chord_of_sin(float s) {
 }
 
 // Per-wave culling of primary rays (V.np >= kConeMin; all 64 lanes must be active).  The wave's rays go
-// from the eye through the screen points of its 8 x 8 block, all within R = 3.5 sqrt(2) pitch of the
-// block centre c, hence (exact geometry) within angle asin(R / |c - eye|) of a = unit(c - eye): chord
+// from the eye through the screen points of its bw x bh block, all within R = half_diag pitch of the
+// block centre c (half_diag = |((bw - 1) / 2, (bh - 1) / 2)|), hence (exact geometry) within angle asin(R / |c - eye|) of a = unit(c - eye): chord
 // distance |u - a| <= rho.  A ray that hits sphere k has |u - v_k| <= chord_k (DevSphereCone, rounded
 // up, radius inflated for FP64 rounding), so |a - v_k| <= rho + chord_k + slack, where `slack` (host,
 // RenderParams) bounds the FP32 error of a and of the test itself.  Lane j evaluates sphere j; the
@@ -536,13 +536,13 @@ __device__ __host__ __forceinline__ float chord_of_sin(float s) {
 __device__ __forceinline__ uint64_t primary_cone_mask(const SceneView& V, const float look[3],
                                                       const float right[3], const float upp[3],
                                                       const float eye[3], float pitch, float ci, float cj,
-                                                      float slack, int lane) {
+                                                      float half_diag, float slack, int lane) {
     const float a_r = pitch * ci, a_u = pitch * cj;
     float dx = fmaf(a_u, upp[0], fmaf(a_r, right[0], look[0])) - eye[0];
     float dy = fmaf(a_u, upp[1], fmaf(a_r, right[1], look[1])) - eye[1];
     float dz = fmaf(a_u, upp[2], fmaf(a_r, right[2], look[2])) - eye[2];
     const float dn = sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz)));
-    const float sn = (3.5f * 1.41422f * 1.001f) * pitch / dn;
+    const float sn = (half_diag * 1.001f) * pitch / dn;
     if (!(sn < 0.5f)) return ~0ull;                         // eye too close to the screen: no culling
     const float rho = chord_of_sin(sn) + slack;
     dx /= dn, dy /= dn, dz /= dn;
@@ -779,9 +779,7 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
 template <bool FULL, bool CULL>
 __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, int mat, d3 u, d3 rdir) {
     const DevScene* S = V.S;
-    const DevMat& M = S->mat[mat];
-    d3 amb = ld3(M.amb), dif = ld3(M.diff), spc = ld3(M.spec);
-    double ks = fabs(dot(u, rdir));
+    const double ks = fabs(dot(u, rdir));
     d3 color = mk(0.0, 0.0, 0.0);
     Ray sr;
     sr.p0 = p;
@@ -792,14 +790,16 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
         double dl;                                          // shadowRay.length()
         d3 sdir = unit(sd, &dl);                            // shadowRay.direction()
         set_dir(&sr, sd, sdir);
+        const double kd = fabs(dot(n, sdir));               // before the shadow test: fewer live registers
         uint64_t m = ~0ull;
         if (CULL && !FULL && V.np >= kConeMin) m = shadow_bundle_mask(V, hit, sr, i);
         bool lit = false;
         if (hit) lit = !(FULL ? occluded_transparent(V, sr) : occluded<false, CULL>(V, sr, i, m));
         if (lit) {
+            const DevMat& M = S->mat[mat];                  // material terms loaded only when lit
             double a = S->att / (S->att + dl * dl);         // attenuation (:1181)
             d3 lC = scl(a, ld3(S->light[i].col));           // :1223
-            d3 term = add(add(had(amb, lC), scl(fabs(dot(n, sdir)), had(dif, lC))), scl(ks, had(spc, lC)));
+            d3 term = add(add(had(ld3(M.amb), lC), scl(kd, had(ld3(M.diff), lC))), scl(ks, had(ld3(M.spec), lC)));
             color = add(color, term);                       // :1224-1226
         }
     }
