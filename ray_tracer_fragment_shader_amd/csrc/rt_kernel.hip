@@ -61,7 +61,6 @@ struct RenderParams {
     int32_t np;
     int32_t nl;
     int32_t wg_staging;                        // 1: stage the 32 x 8 tile in LDS behind a workgroup barrier
-    int32_t wave_w;                            // a wave's block: wave_w x (64 / wave_w) pixels (8, 16 or 32)
     float look32[3], right32[3], upp32[3], eye32[3], pitch32;   // FP32 camera for primary_cone_mask
     float cone_slack;                          // its error bound (render_params)
 };
@@ -117,12 +116,12 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
     const d3 eye = ld3(P.eye);
 
     const int wave = tid >> 6, lane = tid & 63;
-    // The 32 x 8 tile is cut into 4 wave blocks of bw x bh = 64 pixels: 8 x 8 (square: coherent rays) or
-    // wider (16 x 4, 32 x 2: longer contiguous row segments per store).
-    const int bw = P.wave_w, bh = 64 / bw, wpr = kTileW / bw;           // waves per tile row
-    const int bx0 = (wave % wpr) * bw, by0 = (wave / wpr) * bh;
-    const int cx = bx0 + lane % bw;                // column inside the 32 x 8 tile
-    const int cy = by0 + lane / bw;                // row inside the tile
+    // The 32 x 8 tile is cut into 4 wave blocks of 8 x 8 pixels (square blocks keep a wave's rays
+    // coherent; 16 x 4 and 32 x 2 blocks measured no faster, and 32 x 2 slower at c5).
+    constexpr int bw = 8, bh = 8;
+    const int bx0 = wave * bw, by0 = 0;
+    const int cx = bx0 + (lane & 7);               // column inside the 32 x 8 tile
+    const int cy = lane >> 3;                      // row inside the tile
     const int tiles_x = (P.width + kTileW - 1) / kTileW;
     const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
     const int i = tx * kTileW + cx;
@@ -387,7 +386,6 @@ struct rt_ctx {
                                                // despite small spills: tools/ab.py); RT_MIN_WAVES=0 disables
     int use_lds = 0;                           // RT_SCENE_IN_LDS=1: header + exact records in LDS (A/B: tools/ab.py)
     int wg_staging = 0;                        // RT_WG_STAGING=1: LDS-staged 32-pixel row stores (A/B)
-    int wave_w = 8;                            // RT_WAVE_W = 8 | 16 | 32: wave block width (A/B)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -422,10 +420,6 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_SCENE_IN_LDS")) c->use_lds = atoi(e) != 0;
     if (const char* e = getenv("RT_MIN_WAVES")) c->min_waves = atoi(e);
     if (const char* e = getenv("RT_WG_STAGING")) c->wg_staging = atoi(e) != 0;
-    if (const char* e = getenv("RT_WAVE_W")) {
-        const int w = atoi(e);
-        if (w == 8 || w == 16 || w == 32) c->wave_w = w;
-    }
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         delete c;
         return rt_fail(RT_EHIP, "rt_ctx_create: hipEventCreate failed");
@@ -505,7 +499,6 @@ static int render_params(const rt_ctx* c, const rt_camera* cam, int W, int H, in
     P->np = c->n_padded;
     P->nl = c->n_lights;
     P->wg_staging = c->wg_staging;
-    P->wave_w = c->wave_w;
     // FP32 camera for the per-wave cone culling, and the bound on its error as a chord distance: every
     // FP32 coordinate is below M in magnitude and carries < 16 roundings, and |sp - eye| >= |look - eye|
     // (right, up' are orthogonal to look - eye), so direction errors are < 64 eps32 M / |look - eye|.
