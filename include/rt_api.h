@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 #define RT_OK            0
 #define RT_EINVAL       -1   /* bad argument (null pointer, size, unsupported material, ...) */
@@ -200,6 +200,26 @@ int rt_set_scene(rt_ctx* ctx, const rt_scene* scene);
 int rt_render_dev(rt_ctx* ctx, const rt_camera* cam, int width, int height, int depth,
                   const rt_rows* rows, float* rgba32f, uint8_t* rgba8, double* rgb64f,
                   uint32_t* raycount, void* stream);
+
+/* ---- reference-faithful rayTraceScreen ------------------------------- */
+/* rayTraceScreen (MySdlApplication.cpp:1251-1324) exactly as the app runs it: the incremental unit-step
+ * screen walk from (bottom_x, bottom_y) (cam->pitch is not used: the reference steps by the unit vectors
+ * right and up'), every sample jittered by 0.5 * randomUnit() (:1148-1169, rand() arguments evaluated
+ * right to left), up to 16 samples per pixel with the reference's convergence test (:1294-1311), and the
+ * average colour carried from pixel to pixel (:1283).  The carry-over and the shared rand() stream make
+ * the frame a serial chain; the samples are traced on the GPU in speculative chunks (the sample count of
+ * each pixel is predicted, the host resolves the chain in order and re-issues the chunk after the first
+ * wrong prediction), so the result is the reference's, bit for bit.
+ * rand_kind: RT_RAND_GLIBC (glibc rand(), the reference built on Linux) or RT_RAND_MSVC (the MSVC CRT
+ * LCG, the reference's own Visual Studio build); seed as given to srand (the app never calls srand: 1).
+ * Host outputs, each nullable, width*height pixels, j = 0 bottom: rgb64f (the colour passed to
+ * glColor3d, :1312), rgba8 (floor(clamp(c,0,1)*255+0.5)), samples (samples traced per pixel, 2..16);
+ * *rand_calls = rand() calls made.  Synchronous. */
+#define RT_RAND_GLIBC 0
+#define RT_RAND_MSVC  1
+int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, int width, int height,
+                     int depth, int rand_kind, uint32_t seed, double* rgb64f, uint8_t* rgba8,
+                     uint8_t* samples, uint64_t* rand_calls);
 
 /* Synchronous host-buffer convenience: uploads `scene`, renders, copies back, fills *stats
  * (ray counts + kernel time).  Any output pointer may be NULL. */

@@ -56,6 +56,11 @@ def oracle() -> ctypes.CDLL:
         L.oracle_convert_string_coordinate.argtypes = [c_char_p, c_void_p]
         L.oracle_fnv1a64.restype = c_uint64
         L.oracle_fnv1a64.argtypes = [c_void_p, c_size_t]
+        L.oracle_render_screen.restype = c_int
+        L.oracle_render_screen.argtypes = [POINTER(abi.rt_scene), c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                           c_int, c_int, c_int, ctypes.c_uint32, c_void_p, c_void_p, c_void_p]
+        L.oracle_rand_sequence.restype = None
+        L.oracle_rand_sequence.argtypes = [c_int, ctypes.c_uint32, c_int, c_void_p]
         _oracle = L
     return _oracle
 
@@ -85,6 +90,8 @@ def ref() -> ctypes.CDLL:
                                     c_void_p, c_void_p, c_void_p]
         L.ref_convert_string_coordinate.restype = None
         L.ref_convert_string_coordinate.argtypes = [c_char_p, c_void_p]
+        L.ref_screen_rand_calls.restype = c_uint64
+        L.ref_screen_rand_calls.argtypes = scene_args + [c_int, c_int, c_int, c_int, ctypes.c_uint, c_uint64]
         _ref = L
     return _ref
 
@@ -165,6 +172,40 @@ def screen_points(cam, width, height, rows=None):
     b = cam.pitch * (js + cam.bottom_y).astype(np.float64)
     sp = (look[None, None, :] + a[None, :, None] * right[None, None, :]) + b[:, None, None] * upp[None, None, :]
     return sp
+
+
+# ------------------------------------------------------------------- reference-faithful rayTraceScreen
+GLIBC, MSVC = 0, 1       # rand() generators (oracle_render_screen)
+CAMERA = ((0.0, 100.0, 200.0), (0.0, 0.0, -160.0), (0.0, 1.0, 0.0))   # MSA:38-40
+
+
+def render_screen(scene_abi, width, height, depth=5, rng=GLIBC, seed=1, bottom_x=None, bottom_y=None):
+    """rayTraceScreen as the app runs it (jitter, <= 16 adaptive samples, colour carry-over; serial).
+    Returns (rgb [H, W, 3] as handed to glColor3d, samples [H, W] uint8, rand() calls)."""
+    bx = -(width // 2) if bottom_x is None else bottom_x
+    by = -(height // 2) if bottom_y is None else bottom_y
+    eye, look, up = (np.array(v, np.float64) for v in CAMERA)
+    rgb = np.zeros((height, width, 3), np.float64)
+    ns = np.zeros((height, width), np.uint8)
+    calls = c_uint64()
+    rc = oracle().oracle_render_screen(ctypes.byref(scene_abi), _ptr(eye), _ptr(look), _ptr(up), bx, by, width,
+                                       height, depth, rng, seed, _ptr(rgb), _ptr(ns), ctypes.byref(calls))
+    if rc:
+        raise RuntimeError(f"oracle_render_screen failed: {rc}")
+    return rgb, ns, int(calls.value)
+
+
+def rand_sequence(rng, seed, n):
+    out = np.zeros(n, np.int32)
+    oracle().oracle_rand_sequence(rng, seed, n, _ptr(out))
+    return out
+
+
+def ref_screen_rand_calls(scene, width, height, bottom_x=None, bottom_y=None, seed=1, max_calls=1 << 32):
+    """rand() calls made by the reference's own rayTraceScreen on this frame (glibc rand, MAX_DEPTH)."""
+    bx = -(width // 2) if bottom_x is None else bottom_x
+    by = -(height // 2) if bottom_y is None else bottom_y
+    return int(ref().ref_screen_rand_calls(*scene.ref_args(), width, height, bx, by, seed, max_calls))
 
 
 # ------------------------------------------------------------------------------------- reference build

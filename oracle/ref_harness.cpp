@@ -159,6 +159,31 @@ int ref_intersect(const char* children, int n_children, const double* sph_yoff, 
     return 0;
 }
 
+// The reference's own rayTraceScreen (:1251-1324) on the draw() camera (:1552-1560), rand() seeded with
+// `seed` (the app never calls srand: seed 1).  Its glBegin/glColor3d/glVertex2i/glEnd go to the image's
+// real libGL with no current context, where they do nothing, so the colours are not observable; what is
+// observable is how many rand() calls the frame made: 3 per jittered sample (randomUnit, :1148-1169),
+// i.e. the sample counts the convergence test and the colour carry-over produced.  The count is found
+// by locating the next three outputs in the stream restarted from `seed`.
+uint64_t ref_screen_rand_calls(const char* children, int n_children, const double* sph_yoff, const double* sph_r,
+                               const double* mesh_edge, const char* light_sq, const double* light_col,
+                               int n_lights, int W, int H, int bottom_x, int bottom_y, unsigned seed,
+                               uint64_t max_calls) {
+    RefScene rs = build(children, n_children, sph_yoff, sph_r, mesh_edge, light_sq, light_col, n_lights);
+    srand(seed);
+    rayTraceScreen(*rs.scene, rs.lights, Point(CAMERA_POSITION), Point(LOOK_AT_VECTOR), Point(UP_VECTOR),
+                   bottom_x, bottom_y, W, H);
+    int a = rand(), b = rand(), c = rand();
+    delete rs.scene;
+    srand(seed);
+    int x0 = rand(), x1 = rand(), x2 = rand();
+    for (uint64_t n = 0; n < max_calls; ++n) {
+        if (x0 == a && x1 == b && x2 == c) return n;
+        x0 = x1; x1 = x2; x2 = rand();
+    }
+    return ~0ull;
+}
+
 // convertStringCoordinate (:1326-1346).
 void ref_convert_string_coordinate(const char* sq, double out[3]) {
     Point p = convertStringCoordinate(string(sq, 2));

@@ -584,3 +584,118 @@ uint64_t oracle_fnv1a64(const void* data, size_t n) {
     for (size_t i = 0; i < n; ++i) { h ^= p[i]; h *= 1099511628211ULL; }
     return h;
 }
+
+/* ---------------------------------------------- reference-faithful rayTraceScreen
+ * rayTraceScreen (:1251-1324) as the app runs it: incremental screen walk (screenPt += right per pixel,
+ * -= width*right, += up per row), every sample jittered by 0.5 * randomUnit() (:1148-1169), up to
+ * SUPER_SAMPLE_NUMBER = 16 samples with the reference's convergence test (:1294-1311), and avgColor
+ * carried from pixel to pixel (declared once, :1283).  Serial by construction: the sample count of a
+ * pixel depends on its colours and on the carried average, and the rand() stream position of every
+ * later sample depends on all earlier counts.
+ * rand(): rng_kind 0 = glibc's rand() (TYPE_3 additive feedback generator, RAND_MAX = 2^31 - 1) — what
+ * the reference compiled here uses; 1 = the MSVC CRT's LCG (RAND_MAX = 32767) — the reference's own
+ * platform (Visual Studio project).  randomUnit's Point(rand, rand, rand) arguments are evaluated right
+ * to left (z first) by both g++ and MSVC.  Outputs: rgb = the colour handed to glColor3d (:1312),
+ * nsamples = samples traced per pixel, *rand_calls = rand() calls made. */
+typedef struct { int kind; uint32_t lcg; int32_t r[34]; int i; } Rng;
+
+static void rng_seed(Rng* g, int kind, uint32_t seed) {
+    g->kind = kind;
+    g->lcg = seed;
+    if (kind == 0) {                                         /* glibc srandom_r, TYPE_3 */
+        int32_t r[344];
+        r[0] = (int32_t)(seed ? seed : 1);
+        for (int i = 1; i < 31; ++i) {
+            int64_t v = (16807LL * r[i - 1]) % 2147483647LL;
+            r[i] = (int32_t)(v < 0 ? v + 2147483647LL : v);
+        }
+        for (int i = 31; i < 34; ++i) r[i] = r[i - 31];
+        for (int i = 34; i < 344; ++i) r[i] = (int32_t)((uint32_t)r[i - 31] + (uint32_t)r[i - 3]);
+        for (int i = 0; i < 34; ++i) g->r[i] = r[310 + i];
+        g->i = 0;                                            /* g->r holds r[k .. k+33], oldest first */
+    }
+}
+
+static int rng_next(Rng* g) {
+    if (g->kind == 1) {
+        g->lcg = g->lcg * 214013u + 2531011u;
+        return (int)((g->lcg >> 16) & 0x7fff);
+    }
+    int32_t v = (int32_t)((uint32_t)g->r[(g->i + 3) % 34] + (uint32_t)g->r[(g->i + 31) % 34]);
+    g->r[g->i] = v;                                          /* replaces r[k], the oldest */
+    g->i = (g->i + 1) % 34;
+    return (int)((uint32_t)v >> 1);
+}
+
+static double rng_max(const Rng* g) { return g->kind == 1 ? 32767.0 : 2147483647.0; }
+
+/* randomUnit (:1148-1169) */
+static P random_unit(Rng* g, uint64_t* calls) {
+    P v = pt(0.0, 0.0, 0.0);
+    const double den = rng_max(g) + 1.0;
+    while (is_zero(v)) {
+        double z = (double)rng_next(g) / den - .5;          /* arguments evaluated right to left */
+        double y = (double)rng_next(g) / den - .5;
+        double x = (double)rng_next(g) / den - .5;
+        *calls += 3;
+        v = pt(x, y, z);
+    }
+    return nrm(v);
+}
+
+int oracle_render_screen(const rt_scene* d, const double eye[3], const double look[3], const double up[3],
+                         int bottom_x, int bottom_y, int W, int H, int depth, int rng_kind, uint32_t seed,
+                         double* rgb, uint8_t* nsamples, uint64_t* rand_calls) {
+    if (!d || !eye || !look || !up || W <= 0 || H <= 0 || depth < 0 || (rng_kind != 0 && rng_kind != 1))
+        return RT_EINVAL;
+    Scene s;
+    int rc = scene_build(d, &s);
+    if (rc) { scene_free(&s); return rc; }
+    Rng g;
+    rng_seed(&g, rng_kind, seed);
+    uint64_t calls = 0;
+    const double SSN = 16.0;                                 /* SUPER_SAMPLE_NUMBER (:52) */
+    P camera = from3(eye), lookAt = from3(look), upv = from3(up);
+    P lookDirection = sub(lookAt, camera);                   /* :1270 */
+    P right = nrm(cross(lookDirection, upv));                /* :1271-1273 */
+    P rightOffset = scl((double)W, right);                   /* :1274 */
+    P upn = nrm(cross(right, lookDirection));                /* :1276-1277 */
+    P screenPt = add(add(lookAt, scl((double)bottom_x, right)), scl((double)bottom_y, upn));   /* :1279 */
+    P avgColor = pt(0.0, 0.0, 0.0);                          /* :1283, never reset */
+    for (int j = 0; j < H; j++) {
+        for (int i = 0; i < W; i++) {
+            double k;
+            int n = 0;
+            for (k = 0.0; k < SSN; k++) {
+                Line ray;
+                ray.s = camera;
+                ray.e = add(screenPt, scl(.5, random_unit(&g, &calls)));   /* :1296 */
+                P color = pt(0.0, 0.0, 0.0);
+                Count cnt = {0, 0};
+                ray_trace_ray(&s, ray, &color, (unsigned)depth, &cnt);
+                ++n;
+                P oldWeightedColor = scl(k + 1.0, avgColor);
+                avgColor = add(avgColor, color);
+                P weightedColor = scl(k, avgColor);
+                if (len(sub(weightedColor, oldWeightedColor)) < d->small_number * k * (k + 1)) break;
+            }
+            avgColor = pt(avgColor.x / k, avgColor.y / k, avgColor.z / k);   /* :1310 */
+            size_t px = (size_t)j * W + i;
+            if (rgb) { rgb[3 * px] = avgColor.x; rgb[3 * px + 1] = avgColor.y; rgb[3 * px + 2] = avgColor.z; }
+            if (nsamples) nsamples[px] = (uint8_t)n;
+            screenPt = add(screenPt, right);                 /* :1315 */
+        }
+        screenPt = sub(screenPt, rightOffset);               /* :1320 */
+        screenPt = add(screenPt, upn);                       /* :1321 */
+    }
+    if (rand_calls) *rand_calls = calls;
+    scene_free(&s);
+    return RT_OK;
+}
+
+/* The rand() generators alone (tests check them against the C library and the published MSVC LCG). */
+void oracle_rand_sequence(int rng_kind, uint32_t seed, int n, int32_t* out) {
+    Rng g;
+    rng_seed(&g, rng_kind, seed);
+    for (int i = 0; i < n; ++i) out[i] = rng_next(&g);
+}

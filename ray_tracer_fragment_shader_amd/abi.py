@@ -23,6 +23,7 @@ RT_MAX_SPHERES = 1024
 RT_MAX_LIGHTS = 16
 RT_MAX_MESHES = 64
 RT_MAX_DEPTH = 7
+RT_RAND_GLIBC, RT_RAND_MSVC = 0, 1
 RT_MESH_TETRAHEDRON = 1
 RT_MESH_CUBE = 2
 
@@ -121,6 +122,8 @@ SIGNATURES = {
     "rt_trace_rays_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "rt_unshuffle_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "rt_write_ppm": (c_int, [c_char_p, _P(c_uint8), c_int, c_int, c_int]),
+    "rt_render_screen": (c_int, [c_void_p, _P(rt_scene), _P(rt_camera), c_int, c_int, c_int, c_int, ctypes.c_uint32,
+                                 c_void_p, c_void_p, c_void_p, _P(ctypes.c_uint64)]),
     # include/rt_diag.h
     "rt_probe_math_dev": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p]),
 }
@@ -140,7 +143,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.rt_abi_version() != 2:
+        if L.rt_abi_version() != 3:
             raise RuntimeError("librt_amd.so ABI version mismatch")
         _lib = L
     return _lib

@@ -10,6 +10,9 @@
 //   rt_render --config demo --out demo.ppm        initScene's demo (tetrahedron, sphere, cube), 500x500
 //   rt_render --stdin --width 500 --height 500 --pitch 1 --out app.ppm < answers.txt
 //                                                  initScene2's questions answered on stdin
+//   rt_render --config demo --faithful glibc|msvc [--seed S] --out demo_ref.ppm
+//                                                  rayTraceScreen exactly as the app runs it (jitter, up to
+//                                                  16 adaptive samples, colour carry-over): rt_render_screen
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -28,6 +31,8 @@ struct Options {
     bool from_stdin = false;
     int width = 0, height = 0, depth = -1, device = 0;
     double pitch = 0;
+    int faithful = -1;                       // RT_RAND_GLIBC / RT_RAND_MSVC: rt_render_screen
+    unsigned seed = 1;
 };
 
 [[noreturn]] void die(const std::string& what, int code) {
@@ -102,8 +107,11 @@ int main(int argc, char** argv) {
         else if (a == "--depth") o.depth = std::atoi(next().c_str());
         else if (a == "--pitch") o.pitch = std::atof(next().c_str());
         else if (a == "--device") o.device = std::atoi(next().c_str());
+        else if (a == "--faithful") o.faithful = next() == "msvc" ? RT_RAND_MSVC : RT_RAND_GLIBC;
+        else if (a == "--seed") o.seed = (unsigned)std::strtoul(next().c_str(), nullptr, 10);
         else { std::fprintf(stderr, "usage: rt_render [--config c1|c2|c3|c5|demo | --stdin] [--width W --height H "
-                                    "--pitch P --depth B] [--device N] [--out file.ppm]\n"); return 2; }
+                                    "--pitch P --depth B] [--device N] [--faithful glibc|msvc [--seed S]] "
+                                    "[--out file.ppm]\n"); return 2; }
     }
 
     rt_scene scene;
@@ -190,6 +198,20 @@ int main(int argc, char** argv) {
     rt_ctx* ctx = nullptr;
     check(rt_ctx_create(o.device, &ctx), "rt_ctx_create");
     std::vector<uint8_t> rgba8((size_t)W * H * 4);
+    if (o.faithful >= 0) {
+        uint64_t calls = 0;
+        std::vector<uint8_t> ns((size_t)W * H);
+        check(rt_render_screen(ctx, &scene, &cam, W, H, depth, o.faithful, o.seed, nullptr, rgba8.data(), ns.data(),
+                               &calls), "rt_render_screen");
+        check(rt_write_ppm(o.out.c_str(), rgba8.data(), W, H, 4), "rt_write_ppm");
+        unsigned long long samples = 0;
+        for (uint8_t v : ns) samples += v;
+        std::printf("rt_render: %dx%d depth %d faithful rayTraceScreen (%s rand, seed %u) -> %s | %llu samples, "
+                    "%llu rand() calls\n", W, H, depth, o.faithful == RT_RAND_MSVC ? "msvc" : "glibc", o.seed,
+                    o.out.c_str(), samples, (unsigned long long)calls);
+        rt_ctx_destroy(ctx);
+        return 0;
+    }
     rt_stats st;
     check(rt_render(ctx, &scene, &cam, W, H, depth, nullptr, nullptr, rgba8.data(), nullptr, &st), "rt_render");
     check(rt_write_ppm(o.out.c_str(), rgba8.data(), W, H, 4), "rt_write_ppm");

@@ -18,3 +18,9 @@ def frames(cfg_name):
 
 def kat(scene_name):
     return dict(np.load(os.path.join(GOLDEN, f"kat_{scene_name}.npz")))
+
+
+def screen():
+    """Reference-faithful rayTraceScreen pins (tests/golden/make_golden_screen.py)."""
+    with open(os.path.join(GOLDEN, "screen.json")) as f:
+        return json.load(f)

@@ -431,3 +431,50 @@ def test_primary_cone_culling_random_cameras(tr, seed):
     want, want_rc = po.render(sc.to_abi(), cam, W, H, 1)
     _assert_parity(got, want)
     assert np.array_equal(rc, want_rc)
+
+
+def _render_screen(tr, scene, W, H, depth, rng, seed, bx=None, by=None):
+    from ray_tracer_fragment_shader_amd import scenes as S
+    cam = S.make_camera(W, H, 1.0)
+    if bx is not None:
+        cam.bottom_x, cam.bottom_y = bx, by
+    rgb = np.zeros((H, W, 3), np.float64)
+    rgba8 = np.zeros((H, W, 4), np.uint8)
+    ns = np.zeros((H, W), np.uint8)
+    calls = ctypes.c_uint64()
+    abi.check(abi.lib().rt_render_screen(tr._ctx, ctypes.byref(scene.to_abi()), ctypes.byref(cam), W, H, depth, rng,
+                                         seed, rgb.ctypes.data, rgba8.ctypes.data, ns.ctypes.data,
+                                         ctypes.byref(calls)), "rt_render_screen")
+    return rgb, rgba8, ns, int(calls.value)
+
+
+@pytest.mark.parametrize("name,W,H,rng,seed", [("c1", 48, 36, 0, 1), ("c2", 64, 36, 1, 1), ("demo", 50, 50, 0, 1),
+                                               ("c2", 40, 30, 0, 7), ("c5", 37, 23, 1, 99), ("demo", 23, 61, 1, 5)])
+def test_render_screen_faithful_vs_oracle(tr, name, W, H, rng, seed):
+    """rt_render_screen (speculative GPU chunks + in-order resolution) equals the serial restatement bit for
+    bit: colours, per-pixel sample counts and rand() consumption; glibc cases also equal the reference's
+    own rand() consumption (tests/golden/screen.json)."""
+    sc = scenes.CONFIGS[name].scene()
+    rgb, rgba8, ns, calls = _render_screen(tr, sc, W, H, 5, rng, seed)
+    want_rgb, want_ns, want_calls = po.render_screen(sc.to_abi(), W, H, 5, rng, seed)
+    assert np.array_equal(ns, want_ns)
+    assert calls == want_calls
+    assert np.array_equal(rgb, want_rgb)
+    q = np.floor(np.clip(want_rgb, 0.0, 1.0) * 255.0 + 0.5).astype(np.uint8)
+    assert np.array_equal(rgba8[..., :3], q) and (rgba8[..., 3] == 255).all()
+    for g in golden.screen()["cases"]:
+        if (g["scene"], g["width"], g["height"], g["seed"], rng) == (name, W, H, seed, 0):
+            assert calls == g["calls"]
+
+
+def test_cli_faithful_screen_ppm(tmp_path):
+    """`rt_render --config demo --faithful msvc`: the app's rayTraceScreen frame through rt_render_screen."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(abi.LIB_PATH), "rt_render")
+    out = tmp_path / "demo_faithful.ppm"
+    r = subprocess.run([exe, "--config", "demo", "--faithful", "msvc", "--seed", "3", "--width", "64", "--height",
+                        "48", "--out", str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    want, ns, calls = po.render_screen(scenes.CONFIGS["demo"].scene().to_abi(), 64, 48, 5, po.MSVC, 3)
+    assert f"{int(ns.sum())} samples, {calls} rand() calls" in r.stdout
+    assert np.array_equal(_read_ppm(out), _ppm_expect(want))

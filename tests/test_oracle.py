@@ -120,3 +120,40 @@ def test_random_mesh_scenes_vs_reference(seed):
     want = po.ref_render(sc, W, H, depth, 500.0 / W)
     got, _ = po.render(sc.to_abi(), scenes.make_camera(W, H, 500.0 / W), W, H, depth)
     assert np.array_equal(got, want, equal_nan=True)
+
+
+# ------------------------------------------------ reference-faithful rayTraceScreen
+def test_rand_generators():
+    """oracle's rand(): glibc's (the C library here) and the MSVC CRT LCG (published sequence for seed 1)."""
+    import ctypes
+    libc = ctypes.CDLL("libc.so.6")
+    for seed in (1, 7, 12345, 0xDEADBEEF):
+        libc.srand(ctypes.c_uint(seed))
+        want = [libc.rand() for _ in range(2000)]
+        assert list(po.rand_sequence(po.GLIBC, seed, 2000)) == want
+    assert list(po.rand_sequence(po.MSVC, 1, 5)) == [41, 18467, 6334, 26500, 19169]
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_screen_faithful_pinned_to_reference_rand_calls(case):
+    """The serial restatement consumes rand() exactly like the reference's rayTraceScreen (golden pins
+    from the reference build): per frame and per pixel of the bottom row."""
+    g = golden.screen()["cases"][case]
+    sc = scenes.CONFIGS[g["scene"]].scene()
+    W, H = g["width"], g["height"]
+    rgb, ns, calls = po.render_screen(sc.to_abi(), W, H, 5, po.GLIBC, g["seed"], g["bottom_x"], g["bottom_y"])
+    assert calls == g["calls"]
+    assert calls == 3 * int(ns.sum())               # no isZero retry in these frames
+    row0 = [3 * int(ns[0, :k].sum()) for k in range(1, len(g["row0_calls"]) + 1)]
+    assert row0 == g["row0_calls"]
+    assert ns.min() >= 2 and ns.max() == 16 and np.isfinite(rgb).all()
+
+
+@pytest.mark.ref
+@pytest.mark.parametrize("name,W,H,seed", [("c1", 33, 21, 3), ("demo", 41, 29, 1), ("c3", 30, 20, 11)])
+def test_screen_faithful_vs_reference_build(name, W, H, seed):
+    if not po.ref_available():
+        pytest.skip("no reference build here")
+    sc = scenes.CONFIGS[name].scene()
+    _, _, calls = po.render_screen(sc.to_abi(), W, H, 5, po.GLIBC, seed)
+    assert calls == po.ref_screen_rand_calls(sc, W, H, seed=seed)

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Time the reference-faithful rayTraceScreen: rt_render_screen (GPU chunks) vs the serial C restatement
+(oracle/rt_oracle.c, one core — the frame is a serial chain).  usage: screen_bench.py [scene W H ...]"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from oracle import pyoracle as po  # noqa: E402
+from ray_tracer_fragment_shader_amd import abi, scenes  # noqa: E402
+from ray_tracer_fragment_shader_amd.tracer import Tracer  # noqa: E402
+
+
+def main():
+    args = sys.argv[1:] or ["demo", "500", "500", "c2", "640", "360"]
+    tr = Tracer(0)
+    for k in range(0, len(args), 3):
+        name, W, H = args[k], int(args[k + 1]), int(args[k + 2])
+        sc = scenes.CONFIGS[name].scene()
+        sa = sc.to_abi()
+        cam = scenes.make_camera(W, H, 1.0)
+        rgb = np.zeros((H, W, 3), np.float64)
+        ns = np.zeros((H, W), np.uint8)
+        calls = ctypes.c_uint64()
+        t = time.perf_counter()
+        abi.check(abi.lib().rt_render_screen(tr._ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, 5, 0, 1,
+                                             rgb.ctypes.data, None, ns.ctypes.data, ctypes.byref(calls)),
+                  "rt_render_screen")
+        t_gpu = time.perf_counter() - t
+        t = time.perf_counter()
+        want, want_ns, want_calls = po.render_screen(sa, W, H, 5, po.GLIBC, 1)
+        t_cpu = time.perf_counter() - t
+        print(json.dumps({"scene": name, "width": W, "height": H, "samples": int(ns.sum()),
+                          "gpu_s": round(t_gpu, 3), "cpu_serial_s": round(t_cpu, 3),
+                          "speedup": round(t_cpu / t_gpu, 2),
+                          "bit_exact": bool(np.array_equal(rgb, want) and calls.value == want_calls)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
