@@ -772,14 +772,13 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
     *pe = add(p, r);                                        // Line(p, p + r)
 }
 
-// Local illumination of one hit over all lights (:1213-1228).  u = incoming ray direction,
-// rdir = reflectedRay().direction().  `hit` marks the lanes whose colour is wanted.  CULL: called by all
+// Local illumination of one hit over all lights (:1213-1228).  ks = |u . rdir|, u = incoming ray
+// direction, rdir = reflectedRay().direction() (:1225).  `hit` marks the lanes whose colour is wanted.  CULL: called by all
 // lanes of the wave, the light loop stays converged for shadow_bundle_mask; otherwise only by hit lanes.
 // FULL: meshes may be present and materials may be transparent (closest-hit shadows, :1219-1221).
 template <bool FULL, bool CULL>
-__device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, int mat, d3 u, d3 rdir) {
+__device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, int mat, double ks) {
     const DevScene* S = V.S;
-    const double ks = fabs(dot(u, rdir));
     d3 color = mk(0.0, 0.0, 0.0);
     Ray sr;
     sr.p0 = p;
@@ -844,6 +843,39 @@ __device__ __forceinline__ void continue_ray(const SceneView& V, int lvl, int ki
     if (TRANSP) mslot[lvl * kSlotStride] = mat;
 }
 
+// One bounce level of the CULL variant, run by all lanes of the wave (ray_bundle_mask and shade's
+// shadow_bundle_mask reduce over it).  Returns false when no lane hit (the bounce loop ends).
+template <int B, bool TRANSP>
+__device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool first, bool alive, d3 bdP, double bdd,
+                                           uint64_t cone, Ray* r, int* levels, uint32_t* nseg, uint32_t* nsh,
+                                           double* slot, int* mslot) {
+    uint64_t smask = ~0ull;
+    if (!first) {
+        set_origin_f32(V.S, r);
+        if (V.np >= kConeMin) smask = ray_bundle_mask(V, alive, *r);
+    }
+    d3 p = mk(0.0, 0.0, 0.0);
+    int kind = -1;
+    if (alive) {
+        ++*nseg;
+        kind = first ? closest_hit_primary<TRANSP>(V, *r, bdP, bdd, cone, &p) : closest_hit<TRANSP, true>(V, *r, &p, smask);
+    }
+    const bool hit = kind >= 0;
+    if (!__any(hit)) return false;
+    d3 n = mk(0.0, 0.0, 0.0), pe = n, rd = n;
+    int mat = 0;
+    double ks = 0.0;
+    if (hit) {
+        surface(V, kind, p, r->u, &n, &mat, &pe);
+        rd = sub(pe, p);                                    // reflectedRay = Line(p, p + r)
+        ks = fabs(dot(r->u, unit(rd)));                     // |u . reflectedRay.direction()|
+    }
+    const d3 c = shade<TRANSP, true>(V, hit, p, n, mat, ks);
+    // rdir is recomputed (same operations, same bits) rather than kept live through the light loop.
+    if (hit) continue_ray<B, TRANSP>(V, lvl, kind, mat, p, n, rd, unit(rd), c, r, levels, nsh, slot, mslot);
+    return true;
+}
+
 template <int B, bool PRIMARY, bool TRANSP, bool CULL>
 __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, double bdd, uint64_t cone,
                                     uint32_t* seg, uint32_t* shadow, double* slot, int* mslot) {
@@ -860,31 +892,8 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
         if (!__any(alive)) break;                           // the whole wave has missed: early out
         const bool first = PRIMARY && lvl == 0;
         if (CULL) {
-            // All lanes stay in the level body: ray_bundle_mask and shade's shadow_bundle_mask reduce over
-            // the wave.
-            uint64_t smask = ~0ull;
-            if (!first) {
-                set_origin_f32(S, &r);
-                if (V.np >= kConeMin) smask = ray_bundle_mask(V, alive, r);
-            }
-            d3 p = mk(0.0, 0.0, 0.0);
-            int kind = -1;
-            if (alive) {
-                ++nseg;
-                kind = first ? closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p)
-                             : closest_hit<TRANSP, true>(V, r, &p, smask);
-            }
-            const bool hit = kind >= 0;
-            if (!__any(hit)) break;
-            d3 n = mk(0.0, 0.0, 0.0), pe = n, rd = n, rdir = n;
-            int mat = 0;
-            if (hit) {
-                surface(V, kind, p, r.u, &n, &mat, &pe);
-                rd = sub(pe, p);                            // reflectedRay = Line(p, p + r)
-                rdir = unit(rd);                            // reflectedRay.direction()
-            }
-            const d3 c = shade<TRANSP, true>(V, hit, p, n, mat, r.u, rdir);
-            if (hit) continue_ray<B, TRANSP>(V, lvl, kind, mat, p, n, rd, rdir, c, &r, &levels, &nsh, slot, mslot);
+            if (!cull_level<B, TRANSP>(V, lvl, first, alive, bdP, bdd, cone, &r, &levels, &nseg, &nsh, slot, mslot))
+                break;
         } else if (alive) {
             ++nseg;
             d3 p;
@@ -901,7 +910,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                 surface(V, kind, p, r.u, &n, &mat, &pe);
                 d3 rd = sub(pe, p);                         // reflectedRay = Line(p, p + r)
                 d3 rdir = unit(rd);                         // reflectedRay.direction()
-                const d3 c = shade<TRANSP, false>(V, true, p, n, mat, r.u, rdir);
+                const d3 c = shade<TRANSP, false>(V, true, p, n, mat, fabs(dot(r.u, rdir)));
                 continue_ray<B, TRANSP>(V, lvl, kind, mat, p, n, rd, rdir, c, &r, &levels, &nsh, slot, mslot);
             }
         }
