@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--band-height", type=int, default=0, help="0: auto (equal rows per rank)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the N>1 path on a one-GPU box (every rank on device 0, exchange staged "
+                         "through host memory); the measured path is nccl (= RCCL)")
     ap.add_argument("--profile-kernel-only", action="store_true",
                     help="skip parity/ray-count/cpu legs (for rocprofv3 runs)")
     return ap.parse_args()
@@ -93,9 +96,14 @@ def main() -> int:
     if not torch.cuda.is_available():
         print("bench.py needs a HIP GPU", file=sys.stderr)
         return 2
+    if args.backend == "gloo" and torch.cuda.device_count() == 1:
+        local = 0                                           # rehearsal: all ranks share the one GPU
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
@@ -170,7 +178,10 @@ def main() -> int:
             stream.wait_event(assembled[b])                 # recv8[b] consumed by the assembly of step s-2
             pending[b] = exchange_frames(out8[b].view(world, fl, W, 4), recv8[b], world, async_op=True)
             with torch.cuda.stream(side):
-                pending[b].wait()
+                if pending[b] is not None:
+                    pending[b].wait()
+                else:                                       # host-staged rehearsal: recv8[b] filled on `stream`
+                    side.wait_stream(stream)
                 assemble_on_device(recv8[b], plan, W, image8[b], side)
                 assembled[b].record(side)
         elif world > 1:

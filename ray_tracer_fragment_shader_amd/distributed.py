@@ -50,11 +50,22 @@ class BandPlan:
         return scenes.rows(self.band_height, self.world, rank, self.frames if frames is None else frames)
 
 
+def _host_staged(group=None) -> bool:
+    """gloo over device tensors: the rehearsal of the RCCL path on one GPU (bench.py --backend gloo) stages
+    the exchange through host memory; RCCL moves device memory directly."""
+    return dist.get_backend(group) == "gloo"
+
+
 def gather_slabs(slab: torch.Tensor, world: int, root: int = 0, group=None) -> Optional[List[torch.Tensor]]:
     """Gather every rank's padded slab to `root` (one collective).  Returns the list on root, None elsewhere."""
     if world == 1:
         return [slab]
     rank = dist.get_rank(group)
+    if slab.is_cuda and _host_staged(group):
+        h = slab.cpu()
+        hb = [torch.empty_like(h) for _ in range(world)] if rank == root else None
+        dist.gather(h, gather_list=hb, dst=root, group=group)
+        return [b.to(slab.device) for b in hb] if rank == root else None
     bufs = [torch.empty_like(slab) for _ in range(world)] if rank == root else None
     dist.gather(slab, gather_list=bufs, dst=root, group=group)
     return bufs
@@ -66,6 +77,11 @@ def exchange_frames(local: torch.Tensor, recv: torch.Tensor, world: int, async_o
     rank displays."""
     if world == 1:
         recv.copy_(local)
+        return None
+    if local.is_cuda and _host_staged(group):
+        h = torch.empty(recv.shape, dtype=recv.dtype)
+        dist.all_to_all_single(h, local.cpu(), group=group)
+        recv.copy_(h)
         return None
     return dist.all_to_all_single(recv, local, group=group, async_op=async_op)
 
