@@ -21,7 +21,14 @@
 //    proven error margin shows disc < 0, i.e. the FP64 test would report a miss (sphere_reject32);
 //  * board: m = num/nd and s = A/den, t = B/den are divided only when the sign of the operands leaves the
 //    quotient's sign test open (board_hit);
-//  * bounding sphere: an origin with |o - c|^2 < (R-1)^2 provably passes the cull (bound_pass).
+//  * bounding sphere: an origin with |o - c|^2 < (R-1)^2 provably passes the cull (bound_pass);
+//  * shadow rays: a sphere is tested only if the ray's line through the light can meet it (light-cone
+//    records, occluded);
+//  * per-wave culling (>= kConeMin spheres): spheres no ray of the wave can reach, by a conservative
+//    bound on the wave's rays (primary_cone_mask, ray_bundle_mask, shadow_bundle_mask);
+// and exact arithmetic shortcuts:
+//  * |v| and v / |v| without the scale/fixup steps of the IEEE sequences where they are identities, one
+//    reciprocal shared by the three quotients (unit, len_fast).
 #pragma once
 
 #include <hip/hip_runtime.h>
