@@ -16,6 +16,8 @@ extern "C" {
 /* op 0: for each of n vectors v (3 doubles, device memory) write 9 doubles (device memory):
  *   [0..2] v / |v| and [3] |v| with the compiler's sqrt and division (Point::normalize / length),
  *   [4..7] the same from the render kernel's fast path (unit), [8] its len_fast(v).
+ * op 1: for each of n pairs (a, b) write 2 doubles: a / b (the compiler's IEEE division) and the render
+ * kernel's division with a shared reciprocal (div_core(a, b, rcp_core(b)), used by the checker).
  * Asynchronous on `stream`.  RT_EINVAL for an unknown op or null buffers. */
 int rt_probe_math_dev(int op, const double* in, int n, double* out, void* stream);
 

@@ -104,11 +104,11 @@ __device__ __forceinline__ double div_core(double a, double b, double r) {
 
 __device__ __forceinline__ bool num_fast_ok(double a) { return a == 0.0 || fabs(a) >= 0x1p-500; }
 
+// sqrt(x), bit-identical, with the fast sequence when it applies.
+__device__ __forceinline__ double sqrt_fast(double x) { return sqrt_fast_ok(x) ? sqrt_core(x) : sqrt(x); }
+
 // |a| (= len(a), :174).
-__device__ __forceinline__ double len_fast(d3 a) {
-    double s = a.x * a.x + a.y * a.y + a.z * a.z;
-    return sqrt_fast_ok(s) ? sqrt_core(s) : sqrt(s);
-}
+__device__ __forceinline__ double len_fast(d3 a) { return sqrt_fast(a.x * a.x + a.y * a.y + a.z * a.z); }
 
 // u = a / |a| component-wise (= divs(a, len(a)), :174-175, Line::direction :258-263); *l = |a|.
 __device__ __forceinline__ d3 unit(d3 a, double* l) {
@@ -207,7 +207,7 @@ __device__ __forceinline__ bool bound_pass_dp(const DevScene* S, d3 dP, double d
     double uD = dot(u, dP);
     double disc = uD * uD - dd + S->br2;
     if (disc < 0) return false;
-    double s = uD - sqrt(disc);
+    double s = uD - sqrt_fast(disc);
     return !(fabs(s) < S->eps);
 }
 
@@ -289,7 +289,7 @@ __device__ __forceinline__ bool mesh_bound(const DevMesh& M, d3 p0, d3 u, double
     double uD = dot(u, dP);
     double disc = uD * uD - dd + M.br2;
     if (disc < 0) return false;
-    double s = uD - sqrt(disc);
+    double s = uD - sqrt_fast(disc);
     return !(fabs(s) < eps);
 }
 
@@ -372,7 +372,7 @@ __device__ __forceinline__ bool sphere_hit_dp(d3 dP, double dd, double r2, d3 p0
     double uD = dot(u, dP);                                 // :749
     double disc = uD * uD - dd + r2;                        // :750
     if (disc < 0) return false;                             // :754
-    double s = uD - sqrt(disc);                             // :752
+    double s = uD - sqrt_fast(disc);                             // :752
     if (s < eps) return false;                              // covers |s| < eps (:754) and s < eps (:767)
     *p = add(p0, scl(s, u));                                // :762
     return true;
@@ -728,11 +728,16 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
 }
 
 // Material of a hit (checker parity for the board, :1101-1111).
+// (int)(x / square) for the checker, both quotients sharing one reciprocal r = rcp_core(square) (the
+// compiler's own Newton steps): for |x| in [2^-969, 2^500] and a normal `square` div_core is the IEEE
+// quotient bit for bit (fast paths above); below that the quotient is < 2^-400 and truncates to 0 either
+// way, hit points on the board never exceed it, and NaN stays NaN (converted to 0 either way).
 __device__ __forceinline__ int material_of(const SceneView& V, int kind, d3 p) {
     const DevScene* S = V.S;
     if (kind == 0) {
         d3 q = add(sub(p, ld3(S->coff)), mk(S->half, 0.0, S->half));
-        int squareSum = (int)(q.x / S->square) + (int)(q.z / S->square);
+        const double r = rcp_core(S->square);
+        int squareSum = (int)div_core(q.x, S->square, r) + (int)div_core(q.z, S->square, r);
         return (squareSum & 1) == 0 ? 0 : 1;
     }
     if (kind >= kMeshKind) return V.mesh[(kind - kMeshKind) >> 4].mat;

@@ -244,6 +244,10 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     if (s->n_lights > 0 && !s->lights) return rt_fail(RT_EINVAL, "rt_set_scene: null lights");
     if (!(s->small_number >= 0) || !(s->square_edge_size != 0))
         return rt_fail(RT_EINVAL, "rt_set_scene: bad constants");
+    // The kernel's checker divides by the square size with a shared reciprocal (rt_device.hpp
+    // material_of), exact for sizes in this (generous) range.
+    if (!(std::fabs(s->square_edge_size) >= 0x1p-400 && std::fabs(s->square_edge_size) <= 0x1p+400))
+        return rt_fail(RT_EUNSUPPORTED, "rt_set_scene: square_edge_size outside [2^-400, 2^400]");
     if (s->n_meshes < 0 || s->n_meshes > RT_MAX_MESHES || (s->n_meshes > 0 && !s->meshes))
         return rt_fail(RT_EINVAL, "rt_set_scene: bad meshes");
     int n_tris = 0;

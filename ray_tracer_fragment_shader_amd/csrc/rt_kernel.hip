@@ -310,11 +310,18 @@ __global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* 
 
 // Diagnostics (include/rt_diag.h): the exact-arithmetic fast paths of rt_device.hpp beside the compiler's
 // IEEE sequences, on caller-supplied operands.  op 0: per vector v (3 doubles) -> 9 doubles
-// [divs(v, len(v)), len(v), unit(v), |v| from unit(), len_fast(v)].
+// [divs(v, len(v)), len(v), unit(v), |v| from unit(), len_fast(v)]; op 1: per pair (a, b) -> 2 doubles
+// [a / b, div_core(a, b, rcp_core(b))].
 __global__ __launch_bounds__(kThreads) void rt_probe_math_kernel(int op, const double* __restrict__ in, int n,
                                                                  double* __restrict__ out) {
     const int k = blockIdx.x * kThreads + threadIdx.x;
-    if (k >= n || op != 0) return;
+    if (k >= n) return;
+    if (op == 1) {                                          // (a, b) -> [a / b, div_core(a, b, rcp_core(b))]
+        const double a = in[2 * k], b = in[2 * k + 1];
+        out[2 * k] = a / b;
+        out[2 * k + 1] = div_core(a, b, rcp_core(b));
+        return;
+    }
     const d3 v = mk(in[3 * k], in[3 * k + 1], in[3 * k + 2]);
     double* o = out + 9 * (size_t)k;
     const double l0 = len(v);
@@ -664,7 +671,7 @@ extern "C" int rt_unshuffle_dev(const void* gathered, void* image, int W, int H,
 }
 
 extern "C" int rt_probe_math_dev(int op, const double* in, int n, double* out, void* stream) {
-    if (op != 0) return rt_fail(RT_EINVAL, "rt_probe_math_dev: unknown op");
+    if (op != 0 && op != 1) return rt_fail(RT_EINVAL, "rt_probe_math_dev: unknown op");
     if (n < 0 || (n > 0 && (!in || !out))) return rt_fail(RT_EINVAL, "rt_probe_math_dev: bad buffers");
     if (n == 0) return RT_OK;
     hipLaunchKernelGGL(rt_probe_math_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,

@@ -507,3 +507,28 @@ def test_render_dev_graph_capture(tr):
         g.replay()
     torch.cuda.synchronize()
     assert np.array_equal(bufs["rgb64f"].cpu().numpy(), want)
+
+
+def test_checker_division_fast_path(tr):
+    """div_core(a, b, rcp_core(b)) (the checker's quotients) equals IEEE a / b bit for bit for normal
+    b and |a| in [2^-969, 2^500] (and truncates to the same int everywhere on a board)."""
+    import torch
+    rng = np.random.default_rng(11)
+    a = np.concatenate([rng.uniform(-400, 400, 20000), rng.uniform(-1, 1, 5000) * 40.0,
+                        np.arange(-400, 401, 40, dtype=np.float64), np.arange(-400, 401, 40) + 1e-13,
+                        np.arange(-400, 401, 40) - 1e-13, np.ldexp(1.0, np.arange(-960, 490, 3)),
+                        -np.ldexp(1.0, np.arange(-960, 490, 3)) * 1.37, [0.0, -0.0, 1e-300, -1e-310]])
+    b = np.concatenate([np.full(len(a) - 40, 40.0), rng.uniform(0.5, 1e3, 40)])
+    pairs = np.ascontiguousarray(np.stack([a, b], axis=1))
+    d = torch.from_numpy(pairs).cuda()
+    out = torch.empty_like(d)
+    abi.check(abi.lib().rt_probe_math_dev(1, ctypes.c_void_p(d.data_ptr()), len(a), ctypes.c_void_p(out.data_ptr()),
+                                          None), "rt_probe_math_dev")
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    ieee = a / b
+    assert np.array_equal(o[:, 0], ieee)
+    regular = (np.abs(a) >= 2.0 ** -969) & (np.abs(a) <= 2.0 ** 500)
+    assert _same_bits(o[regular, 1], ieee[regular]).all()
+    board = np.abs(a) <= 1e4
+    assert np.array_equal(np.trunc(o[board, 1]), np.trunc(ieee[board]))
