@@ -832,15 +832,15 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
 constexpr int kSlotStride = 256;
 
 // A hit at level lvl: park its colour in LDS and turn r into the continuation ray (:1238-1247).
-template <int B, bool TRANSP>
+template <int B, bool TRANSP, int SS = kSlotStride>
 __device__ __forceinline__ void continue_ray(const SceneView& V, int lvl, int kind, int mat, d3 p, d3 n, d3 rd,
                                              d3 rdir, d3 c, Ray* r, int* levels, uint32_t* nsh, double* slot,
                                              int* mslot) {
     const DevScene* S = V.S;
-    double* sl = slot + 3 * lvl * kSlotStride;
+    double* sl = slot + 3 * lvl * SS;
     sl[0] = c.x;
-    sl[kSlotStride] = c.y;
-    sl[2 * kSlotStride] = c.z;
+    sl[SS] = c.y;
+    sl[2 * SS] = c.z;
     *nsh += V.nl;
     *levels = lvl + 1;
     if (TRANSP && S->mat[mat].transmit) {
@@ -852,12 +852,12 @@ __device__ __forceinline__ void continue_ray(const SceneView& V, int lvl, int ki
         r->p0 = p;
         set_dir(r, rd, rdir);
     }
-    if (TRANSP) mslot[lvl * kSlotStride] = mat;
+    if (TRANSP) mslot[lvl * SS] = mat;
 }
 
 // One bounce level of the CULL variant, run by all lanes of the wave (ray_bundle_mask and shade's
 // shadow_bundle_mask reduce over it).  Returns false when no lane hit (the bounce loop ends).
-template <int B, bool TRANSP>
+template <int B, bool TRANSP, int SS = kSlotStride>
 __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool first, bool alive, d3 bdP, double bdd,
                                            uint64_t cone, Ray* r, int* levels, uint32_t* nseg, uint32_t* nsh,
                                            double* slot, int* mslot) {
@@ -884,11 +884,11 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     }
     const d3 c = shade<TRANSP, true>(V, hit, p, n, mat, ks);
     // rdir is recomputed (same operations, same bits) rather than kept live through the light loop.
-    if (hit) continue_ray<B, TRANSP>(V, lvl, kind, mat, p, n, rd, unit(rd), c, r, levels, nsh, slot, mslot);
+    if (hit) continue_ray<B, TRANSP, SS>(V, lvl, kind, mat, p, n, rd, unit(rd), c, r, levels, nsh, slot, mslot);
     return true;
 }
 
-template <int B, bool PRIMARY, bool TRANSP, bool CULL>
+template <int B, bool PRIMARY, bool TRANSP, bool CULL, int SS = kSlotStride>
 __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, double bdd, uint64_t cone,
                                     uint32_t* seg, uint32_t* shadow, double* slot, int* mslot) {
     const DevScene* S = V.S;
@@ -904,7 +904,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
         if (!__any(alive)) break;                           // the whole wave has missed: early out
         const bool first = PRIMARY && lvl == 0;
         if (CULL) {
-            if (!cull_level<B, TRANSP>(V, lvl, first, alive, bdP, bdd, cone, &r, &levels, &nseg, &nsh, slot, mslot))
+            if (!cull_level<B, TRANSP, SS>(V, lvl, first, alive, bdP, bdd, cone, &r, &levels, &nseg, &nsh, slot, mslot))
                 break;
         } else if (alive) {
             ++nseg;
@@ -923,17 +923,17 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                 d3 rd = sub(pe, p);                         // reflectedRay = Line(p, p + r)
                 d3 rdir = unit(rd);                         // reflectedRay.direction()
                 const d3 c = shade<TRANSP, false>(V, true, p, n, mat, fabs(dot(r.u, rdir)));
-                continue_ray<B, TRANSP>(V, lvl, kind, mat, p, n, rd, rdir, c, &r, &levels, &nsh, slot, mslot);
+                continue_ray<B, TRANSP, SS>(V, lvl, kind, mat, p, n, rd, rdir, c, &r, &levels, &nsh, slot, mslot);
             }
         }
     }
     d3 acc = mk(0.0, 0.0, 0.0);
 #pragma unroll 1
     for (int lvl = levels - 1; lvl >= 0; --lvl) {
-        const double* sl = slot + 3 * lvl * kSlotStride;
-        d3 c = mk(sl[0], sl[kSlotStride], sl[2 * kSlotStride]);
+        const double* sl = slot + 3 * lvl * SS;
+        d3 c = mk(sl[0], sl[SS], sl[2 * SS]);
         if (lvl == levels - 1) acc = c;
-        else acc = TRANSP ? add(c, had(ld3(S->mat[mslot[lvl * kSlotStride]].w), acc)) : add(c, acc);
+        else acc = TRANSP ? add(c, had(ld3(S->mat[mslot[lvl * SS]].w), acc)) : add(c, acc);
     }
     *seg = nseg;
     *shadow = nsh;

@@ -1,16 +1,16 @@
 // rt_kernel.hip — MI355X (gfx950) kernels and the device half of the C ABI (include/rt_api.h).
 //
 // Kernels
-//   rt_render_kernel<B, LDS, MINW, TRANSP, CULL>  one work-item per pixel, FP64, iterative bounce loop
+//   rt_render_kernel<B, LDS, MINW, TRANSP, CULL, WG>  one work-item per pixel, FP64, iterative bounce loop
 //                             (rt_device.hpp); CULL: wave-level sphere culling for >= kConeMin spheres.
-//                             Workgroup = 256 work-items = 4 wave64; the workgroup owns a 32 x 8 pixel
-//                             tile and each wave an 8 x 8 sub-tile (square sub-tiles keep a wave's rays
-//                             coherent, so the __any early-out in the bounce loop fires for whole waves).
-//                             The scene (bounding sphere, board, materials, lights, spheres; < 36 KB at
-//                             the 1024-sphere maximum, ~3 KB at 64) is copied into LDS once per
-//                             workgroup (LDS = 1) or read through the scalar cache (LDS = 0).
-//                             Results are staged through LDS and written back as whole 32-pixel rows
-//                             (512 B of RGBA32F per row segment), so framebuffer stores are coalesced.
+//                             Default: one-wave workgroups (WG = 64), each owning an 8 x 8 pixel tile
+//                             (square tiles keep a wave's rays coherent, so the __any early-out and the
+//                             culling masks work for whole waves).  The scene (bounding sphere, board,
+//                             materials, lights, spheres) is read through the scalar cache; the A/B
+//                             variants with 256-thread workgroups (32 x 8 tiles) copy it into LDS once per
+//                             workgroup (LDS = 1) or stage the output tile in LDS for 32-pixel row stores.
+//                             Per-level colours wait in LDS slots; stores go out per wave (8 rows of
+//                             128 B of RGBA32F).
 //   rt_trace_rays_kernel<B>   rayTraceRay on an arbitrary ray list (parity / fuzz entry point).
 //   rt_intersect_kernel       g_scene.intersection on an arbitrary ray list (primitive KATs).
 //   rt_unshuffle_kernel       multi-GPU: gathered row bands -> image order.
@@ -40,9 +40,10 @@ constexpr int kTileH = 8;    // ... x 8 rows = 256 pixels
 constexpr int kThreads = 256;
 static_assert(kThreads == kSlotStride, "one LDS colour slot column per work-item");
 
-// LDS bytes of trace()'s per-level slots for depth B: 3 doubles (+ the material id when TRANSP) per level.
-__host__ __device__ constexpr int slot_bytes(int B, bool transp) {
-    return (B + 1) * (3 * 8 + (transp ? 4 : 0)) * kSlotStride;
+// LDS bytes of trace()'s per-level slots for depth B: 3 doubles (+ the material id when TRANSP) per level
+// and work-item of a `wg`-thread workgroup.
+__host__ __device__ constexpr int slot_bytes(int B, bool transp, int wg = kSlotStride) {
+    return (B + 1) * (3 * 8 + (transp ? 4 : 0)) * wg;
 }
 
 struct RenderParams {
@@ -85,8 +86,8 @@ __device__ __forceinline__ unsigned char to_u8(double c) {
     return (unsigned char)(int)floor(v * 255.0 + 0.5);
 }
 
-template <int B, int LDS, int MINW, bool TRANSP, bool CULL>
-__global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
+template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads>
+__global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
                                                              RenderParams P, float4* __restrict__ out32,
                                                              uchar4* __restrict__ out8,
                                                              double* __restrict__ out64,
@@ -105,8 +106,8 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
         off = P.lds_bytes;
     }
     double* slot = reinterpret_cast<double*>(smem + off) + tid;
-    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * (B + 1) * kSlotStride) + tid;
-    off += slot_bytes(B, TRANSP);
+    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * (B + 1) * WG) + tid;
+    off += slot_bytes(B, TRANSP, WG);
     float4* st32 = reinterpret_cast<float4*>(smem + off);                              // [8][32] 4 KB
     double* st64 = reinterpret_cast<double*>(smem + off + 4096);                        // [8][32][3] 6 KB
     uint32_t* strc = reinterpret_cast<uint32_t*>(smem + off + 4096 + 6144);             // [8][32] 1 KB
@@ -116,15 +117,16 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
     const d3 eye = ld3(P.eye);
 
     const int wave = tid >> 6, lane = tid & 63;
-    // The 32 x 8 tile is cut into 4 wave blocks of 8 x 8 pixels (square blocks keep a wave's rays
-    // coherent; 16 x 4 and 32 x 2 blocks measured no faster, and 32 x 2 slower at c5).
-    constexpr int bw = 8, bh = 8;
+    // The 32 x 8 tile (WG = 256) is cut into 4 wave blocks of 8 x 8 pixels (square blocks keep a wave's
+    // rays coherent; 16 x 4 and 32 x 2 blocks measured no faster, and 32 x 2 slower at c5); WG = 64: one
+    // wave, one 8 x 8 tile.
+    constexpr int bw = 8, bh = 8, TW = WG / 8;
     const int bx0 = wave * bw, by0 = 0;
-    const int cx = bx0 + (lane & 7);               // column inside the 32 x 8 tile
+    const int cx = bx0 + (lane & 7);               // column inside the tile
     const int cy = lane >> 3;                      // row inside the tile
-    const int tiles_x = (P.width + kTileW - 1) / kTileW;
+    const int tiles_x = (P.width + TW - 1) / TW;
     const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
-    const int i = tx * kTileW + cx;
+    const int i = tx * TW + cx;
     const int lr = ty * kTileH + cy;
     const bool valid = i < P.width && lr < P.local_rows;
 
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
         const float hx = 0.5f * (float)(bw - 1), hy = 0.5f * (float)(bh - 1);
         if (one_frame && jb - ja == bh - 1)
             cone = primary_cone_mask(V, P.look32, P.right32, P.upp32, P.eye32, P.pitch32,
-                                     (float)(tx * kTileW + bx0 + P.bottom_x) + hx, (float)(ja + P.bottom_y) + hy,
+                                     (float)(tx * TW + bx0 + P.bottom_x) + hx, (float)(ja + P.bottom_y) + hy,
                                      sqrtf(hx * hx + hy * hy), P.cone_slack, lane);
     }
 
@@ -151,9 +153,9 @@ __global__ __launch_bounds__(kThreads, MINW) void rt_render_kernel(const DevScen
     const d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(ic + P.bottom_x), right)),
                       scl(P.pitch * (double)(j + P.bottom_y), upp));
     const d3 bdP = sub(ld3(V.S->bc), eye);                  // bounding-sphere deltaP for p0 = camera
-    const d3 col = trace<B, true, TRANSP, CULL>(V, eye, sp, bdP, dot(bdP, bdP), cone, &seg, &sh, slot, mslot);
+    const d3 col = trace<B, true, TRANSP, CULL, WG>(V, eye, sp, bdP, dot(bdP, bdP), cone, &seg, &sh, slot, mslot);
 
-    if (!P.wg_staging) {
+    if (WG != kThreads || !P.wg_staging) {
         // Direct stores: each wave writes its 8 x 8 block as 8 row segments (128 B of RGBA32F each) and
         // retires without waiting at a workgroup barrier for slower waves of the tile.
         if (valid) {
@@ -335,17 +337,17 @@ __global__ __launch_bounds__(kThreads) void rt_probe_math_kernel(int op, const d
 
 // ------------------------------------------------------------------------------------------------
 // Template dispatch.
-template <int LDS, int MINW, bool TRANSP, bool CULL = false>
+template <int LDS, int MINW, bool TRANSP, bool CULL = false, int WG = kThreads>
 hipError_t launch_render_lds(int depth, dim3 grid, size_t lds, hipStream_t st, const DevScene* s,
                              const RenderParams& P, float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
 #define RT_CASE(b)                                                                                      \
     case b:                                                                                             \
         if (lds > 65536) {                                                                              \
-            hipError_t e_ = hipFuncSetAttribute((const void*)rt_render_kernel<b, LDS, MINW, TRANSP, CULL>,                  \
+            hipError_t e_ = hipFuncSetAttribute((const void*)rt_render_kernel<b, LDS, MINW, TRANSP, CULL, WG>,                  \
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);  \
             if (e_ != hipSuccess) return e_;                                                            \
         }                                                                                               \
-        hipLaunchKernelGGL((rt_render_kernel<b, LDS, MINW, TRANSP, CULL>), grid, dim3(kThreads), lds, st, s, P, o32, o8,    \
+        hipLaunchKernelGGL((rt_render_kernel<b, LDS, MINW, TRANSP, CULL, WG>), grid, dim3(WG), lds, st, s, P, o32, o8,    \
                            o64, orc);                                                                   \
         break;
     switch (depth) {
@@ -532,10 +534,17 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     if (rc) return rc;
     if (P.local_rows == 0) return RT_OK;
     RT_HIP(hipSetDevice(c->device));
-    const int tiles_x = (W + kTileW - 1) / kTileW;
+    // One-wave workgroups (8 x 8 tiles) by default: measured faster than 256-thread workgroups (32 x 8
+    // tiles) at every config (c2 -1%, c3 -3%, c5 -12%: a finished wave's slot is refilled without
+    // waiting for three siblings).  The A/B variants that share a workgroup-wide LDS copy (scene in LDS,
+    // staged row stores) keep 256 threads.
+    const bool big = c->use_lds || c->wg_staging;
+    const int tw = big ? kTileW : 8;
+    const int tiles_x = (W + tw - 1) / tw;
     const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
     dim3 grid((unsigned)(tiles_x * tiles_y));
-    const size_t stage = (c->wg_staging ? 4096 + 6144 + 1024 + 1024 : 0) + slot_bytes(depth, c->transparent);
+    const size_t lds64 = slot_bytes(depth, c->transparent, 64);
+    const size_t lds256 = (c->wg_staging ? 4096 + 6144 + 1024 + 1024 : 0) + slot_bytes(depth, c->transparent);
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     // Primary-ray sphere data for this eye (stream-ordered; only when the eye changes).
@@ -550,20 +559,22 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
         memcpy(c->eye, cam->eye, sizeof(c->eye));
         c->eye_valid = true;
     }
+    const bool cull = c->n_padded >= kConeMin, mw5 = c->min_waves >= 5 && depth <= 3;
+    float4* o32 = reinterpret_cast<float4*>(rgba32f);
+    uchar4* o8 = reinterpret_cast<uchar4*>(rgba8);
     if (c->transparent)
-        e = launch_render_lds<0, 1, true>(depth, grid, stage, st, c->d_scene, P, reinterpret_cast<float4*>(rgba32f),
-                                          reinterpret_cast<uchar4*>(rgba8), rgb64f, raycount);
+        e = launch_render_lds<0, 1, true, false, 64>(depth, grid, lds64, st, c->d_scene, P, o32, o8, rgb64f, raycount);
     else if (c->use_lds)
-        e = launch_render_lds<1, 1, false>(depth, grid, c->lds_bytes + stage, st, c->d_scene, P,
-                                 reinterpret_cast<float4*>(rgba32f), reinterpret_cast<uchar4*>(rgba8), rgb64f,
-                                 raycount);
+        e = launch_render_lds<1, 1, false, false, kThreads>(depth, grid, c->lds_bytes + lds256, st, c->d_scene, P,
+                                                             o32, o8, rgb64f, raycount);
+    else if (c->wg_staging)
+        e = (mw5 ? launch_render_lds<0, 5, false, false, kThreads> : launch_render_lds<0, 1, false, false, kThreads>)(
+                depth, grid, lds256, st, c->d_scene, P, o32, o8, rgb64f, raycount);
     else {
         // >= kConeMin spheres: the wave-culling variant (secondary and shadow rays, rt_device.hpp CULL).
-        const bool cull = c->n_padded >= kConeMin, mw5 = c->min_waves >= 5 && depth <= 3;
-        auto launch = cull ? (mw5 ? launch_render_lds<0, 5, false, true> : launch_render_lds<0, 1, false, true>)
-                           : (mw5 ? launch_render_lds<0, 5, false, false> : launch_render_lds<0, 1, false, false>);
-        e = launch(depth, grid, stage, st, c->d_scene, P, reinterpret_cast<float4*>(rgba32f),
-                   reinterpret_cast<uchar4*>(rgba8), rgb64f, raycount);
+        auto launch = cull ? (mw5 ? launch_render_lds<0, 5, false, true, 64> : launch_render_lds<0, 1, false, true, 64>)
+                           : (mw5 ? launch_render_lds<0, 5, false, false, 64> : launch_render_lds<0, 1, false, false, 64>);
+        e = launch(depth, grid, lds64, st, c->d_scene, P, o32, o8, rgb64f, raycount);
     }
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_kernel launch: ") + hipGetErrorString(e));
     return RT_OK;

@@ -134,17 +134,23 @@ def test_output_formats_consistent(tr):
     assert np.all(c8[..., 3] == 255)
 
 
-def test_scene_in_lds_and_scalar_cache_agree():
-    cfg = scenes.CONFIGS["c5"]
+@pytest.mark.parametrize("env", ["RT_SCENE_IN_LDS", "RT_WG_STAGING"])
+@pytest.mark.parametrize("name", ["c2", "c5"])
+def test_workgroup_variants_agree(env, name):
+    """The 256-thread A/B variants (scene copied into LDS; LDS-staged row stores) equal the default
+    one-wave-workgroup kernel and the oracle bit for bit."""
+    cfg = scenes.CONFIGS[name]
     W, H = 200, 150
     out = []
     for mode in ("1", "0"):
-        os.environ["RT_SCENE_IN_LDS"] = mode
+        os.environ[env] = mode
         t = Tracer(0)
         out.append(_render64(t, cfg.scene(), cfg.camera(W, H), W, H, cfg.depth)[0])
         t.close()
-    os.environ.pop("RT_SCENE_IN_LDS")
+    os.environ.pop(env)
     assert np.array_equal(out[0], out[1])
+    want, _ = po.render(cfg.scene().to_abi(), cfg.camera(W, H), W, H, cfg.depth)
+    assert np.array_equal(out[1], want)
 
 
 @pytest.mark.parametrize("G,hb", [(2, 8), (3, 5), (8, 16), (4, 1)])
