@@ -8,13 +8,14 @@ parity image) and the RGBA8 display image, all buffers resident in HBM.  Rays ar
 actually-traced count (primary + reflected + shadow), taken from the kernel's own
 per-pixel ray counters before the timed region and checked against the reference's pinned total.
 
-N>1 (torch.distributed.run, one rank per GPU, RCCL): weak scaling by default ("frame streams") — a step
-is N frames, one per rank as its display; every frame is row-banded over all N ranks (round-robin bands, height
-chosen so every rank gets the same rows), each rank renders its bands of all N frames in ONE launch (rt_rows.frames = N), one RCCL
-all-to-all sends frame f's rows to rank f, and rank f puts them in image order with rt_unshuffle_dev.
-Per-GPU work stays one frame; the exchange and the assembly of step s overlap the render of step s+1
-(double-buffered RGBA8 slabs, a side stream).  `--scaling strong` renders ONE frame per step split over
-the N ranks and gathers it to rank 0 (the c4 design).
+N>1 (torch.distributed.run, one rank per GPU): `--scaling weak` (default) — frames are independent units,
+so every rank renders whole frames of its own (one per step) with no data-path collective; the job's rays
+per step are N frames' worth.  `--scaling streams` — N frames per step, each row-banded over all N ranks
+(round-robin bands, equal rows per rank), each rank renders its bands of all N frames in ONE launch
+(rt_rows.frames = N), one RCCL all-to-all sends frame f's rows to rank f, which puts them in image order
+with rt_unshuffle_dev; the exchange and the assembly of step s overlap the render of step s+1
+(double-buffered RGBA8 slabs, a side stream).  `--scaling strong` — ONE frame per step split over the N
+ranks by row bands and gathered to rank 0 over RCCL (north_star's row-partitioned c4 design).
 
 Printed: ONE JSON line on rank 0 (contract in the task statement) with `roofline` (HBM-write roofline of
 the dominant kernel, per north_star) and `roofline_fp64` (its FP64 VALU roofline) and `cpu_baseline`
@@ -45,7 +46,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c5"])
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "streams", "strong"])
     ap.add_argument("--band-height", type=int, default=0, help="0: auto (equal rows per rank)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3)
@@ -118,23 +119,27 @@ def main() -> int:
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream(dev)
 
-    weak = world > 1 and args.scaling == "weak"
-    frames = world if weak else 1
-    plan = BandPlan(H, world, args.band_height, frames=frames)
-    if weak and not plan.balanced:
+    streams = world > 1 and args.scaling == "streams"       # banded frames + all-to-all
+    strong = world > 1 and args.scaling == "strong"         # one banded frame + gather to rank 0
+    banded = streams or strong                              # else: whole frames per rank, no collective
+    frames = world if streams else 1                        # frames stacked in one launch on this rank
+    job_frames = 1 if strong else world                     # frames the whole job renders per step
+    plan = BandPlan(H, world if banded else 1, args.band_height, frames=frames)
+    if streams and not plan.balanced:
         raise SystemExit(f"frame streams need equal rows per rank: H={H}, N={world}, band {plan.band_height}")
-    rows = plan.rows(rank) if world > 1 else None
-    nl = plan.local[rank]                  # rows this rank renders per step (all its frames)
-    fl = plan.frame_local[rank]            # ... per frame
+    prank = rank if banded else 0
+    rows = plan.rows(rank) if banded else None
+    nl = plan.local[prank]                 # rows this rank renders per step (all its frames)
+    fl = plan.frame_local[prank]           # ... per frame
     out32 = torch.empty((nl, W, 4), dtype=torch.float32, device=dev)
     out8 = [torch.empty((nl, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
-    if weak:
+    if streams:
         recv8 = [torch.empty((world, fl, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
         image8 = [torch.empty((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
         side = torch.cuda.Stream(dev)
         assembled = [torch.cuda.Event() for _ in range(2)]
         pending = [None, None]
-    elif world > 1 and rank == 0:
+    elif strong and rank == 0:
         image8 = [torch.empty((H, W, 4), dtype=torch.uint8, device=dev)]
 
     # ---- parity + ray count (outside the timed region) ----------------------------------------------
@@ -169,12 +174,12 @@ def main() -> int:
     def step():
         b = counter[0] % 2
         counter[0] += 1
-        if weak and pending[b] is not None:
+        if streams and pending[b] is not None:
             pending[b].wait()                               # the all-to-all of step s-2 has read out8[b]
         rc = fn(*launch_args[b])
         if rc:
             abi.check(rc, "rt_render_dev")
-        if weak:
+        if streams:
             stream.wait_event(assembled[b])                 # recv8[b] consumed by the assembly of step s-2
             pending[b] = exchange_frames(out8[b].view(world, fl, W, 4), recv8[b], world, async_op=True)
             with torch.cuda.stream(side):
@@ -184,7 +189,7 @@ def main() -> int:
                     side.wait_stream(stream)
                 assemble_on_device(recv8[b], plan, W, image8[b], side)
                 assembled[b].record(side)
-        elif world > 1:
+        elif strong:
             gathered = gather_slabs(out8[b], world)
             if rank == 0:
                 assemble_on_device(torch.stack(gathered), plan, W, image8[0], stream)
@@ -223,7 +228,7 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    rays_step = rays_frame * frames
+    rays_step = rays_frame * job_frames
     value = rays_step * args.steps / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
 
@@ -245,20 +250,22 @@ def main() -> int:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
-            "ms_per_frame": round(ms_step / frames, 4),
+            "ms_per_frame": round(ms_step / job_frames, 4),
             "higher_is_better": True,
-            "scaling": args.scaling if world > 1 else "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: canonical scene of SURVEY.md Appendix B (deterministic, no RNG)",
             "config": {
                 "workload": f"{cfg.name}: {W}x{H}, {cfg.n_spheres} spheres + checkerboard, {cfg.n_lights} light(s), "
-                            f"{B} bounce(s), pitch 500/W; step = {frames} frame(s)",
+                            f"{B} bounce(s), pitch 500/W; step = {job_frames} frame(s)",
                 "width": W, "height": H, "spheres": cfg.n_spheres, "lights": cfg.n_lights, "bounces": B,
-                "rays_per_frame": rays_frame, "frames_per_step": frames,
+                "rays_per_frame": rays_frame, "frames_per_step": job_frames,
                 "parallelism": (f"frame streams: {world} frames/step, row bands (h={plan.band_height}) x {world} "
-                                f"ranks, RCCL all-to-all" if weak else
+                                f"ranks, RCCL all-to-all" if streams else
                                 f"row bands (h={plan.band_height}) x {world} ranks + RCCL gather to rank 0"
+                                if strong else
+                                f"{world} ranks x whole frames (independent frames, no collective)"
                                 if world > 1 else "single GPU"),
             },
             "roofline": {
