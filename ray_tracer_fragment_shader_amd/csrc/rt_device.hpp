@@ -451,7 +451,8 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
 }
 
 // Closest hit of a primary ray Line(eye, sp): deltaP and |deltaP|^2 per sphere were computed for this
-// eye by rt_prepare_kernel with the reference's operations (:740, :750).
+// eye by rt_prepare_kernel with the reference's operations (:740, :750).  A miss of the bounding-sphere
+// cull makes the whole g_scene a miss, whatever the children say, so it can be tested after them.
 // One sphere of a primary ray: FP32 filter on the per-eye image, then the exact test (:747-772) and the
 // strict-< closest-hit update (:811-813).
 __device__ __forceinline__ void primary_sphere(const SceneView& V, const Ray& r, int k, double eps, int* kind,
@@ -474,14 +475,14 @@ __device__ __forceinline__ void primary_sphere(const SceneView& V, const Ray& r,
 }
 
 // Closest hit of a primary ray Line(eye, sp): deltaP and |deltaP|^2 per sphere were computed for this
-// eye by rt_prepare_kernel with the reference's operations (:740, :750).  `cone` (np >= kConeMin): bit k
+// eye by rt_prepare_kernel with the reference's operations (:740, :750).  A miss of the bounding-sphere
+// cull makes the whole g_scene a miss, whatever the children say, so it can be tested after them.  `cone` (np >= kConeMin): bit k
 // set when sphere k < 64 may be hit by some ray of this wave (primary_cone_mask); the others are
 // provably missed and skipped.  Spheres are still visited in increasing k (tie order unchanged).
 template <bool FULL>
 __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray& r, d3 bdP, double bdd,
                                                    uint64_t cone, d3* hp) {
     const DevScene* S = V.S;
-    if (!bound_pass_dp(S, bdP, bdd, r.u)) return -1;
     int kind = -1;
     double best = -1.0;
     if (S->has_board) {
@@ -525,6 +526,9 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
         }
     }
     if (FULL) meshes_closest(V, r, eps, &kind, &best, hp);
+    // The bounding-sphere cull (:747-758) only turns hits into misses, so it is evaluated last and only
+    // for rays that hit something: waves of background rays skip it.
+    if (kind >= 0 && !bound_pass_dp(S, bdP, bdd, r.u)) kind = -1;
     return kind;
 }
 
