@@ -36,6 +36,19 @@
 
 #include "rt_layout.hpp"
 
+// 1: the exact tests of a filter batch visit its spheres in a loop the whole wave runs (record index
+// wave-uniform: scalar loads, SGPR operands; lanes whose filter rejected a sphere are masked off);
+// 0: each lane walks its own surviving spheres (per-lane index: vector loads).
+#ifndef RT_UNIFORM_PRIMARY
+#define RT_UNIFORM_PRIMARY 1
+#endif
+#ifndef RT_UNIFORM_SECONDARY
+#define RT_UNIFORM_SECONDARY 1
+#endif
+#ifndef RT_UNIFORM_SHADOW
+#define RT_UNIFORM_SHADOW 0
+#endif
+
 namespace rt {
 
 struct d3 {
@@ -103,6 +116,17 @@ __device__ __forceinline__ double div_core(double a, double b, double r) {
 }
 
 __device__ __forceinline__ bool num_fast_ok(double a) { return a == 0.0 || fabs(a) >= 0x1p-500; }
+
+// a / b for a constant b with r = rcp_core(b) precomputed on the device (rt_scene_init_kernel).  `fast`
+// (host): |b| in [2^-200, 2^200]; then for |a| in [2^-500, 2^500] the quotient's exponent is within
+// [-700, 700] and exponent(a) - exponent(b) <= 700 < 768, so the sequence's div_scale steps are identities
+// and div_core is the IEEE quotient bit for bit (fast paths above); other operands (zero, tiny, huge,
+// NaN) take the compiler's division.
+__device__ __forceinline__ double div_const(double a, double b, double r, int32_t fast) {
+    const double aa = fabs(a);
+    if (fast && aa >= 0x1p-500 && aa <= 0x1p+500) return div_core(a, b, r);
+    return a / b;
+}
 
 // sqrt(x), bit-identical, with the fast sequence when it applies.
 __device__ __forceinline__ double sqrt_fast(double x) { return sqrt_fast_ok(x) ? sqrt_core(x) : sqrt(x); }
@@ -218,14 +242,16 @@ __device__ __forceinline__ bool bound_pass(const DevScene* S, d3 p0, d3 u) {
 }
 
 // CheckerBoard -> Quad -> Triangle T1 then T2, first hit wins (:1097, :817, :611-707).
-// d = end - start (unnormalised, :647).  Returns the hit point in *p.
+// d = end - start (unnormalised, :647).  Returns the hit point in *p.  PRIMARY: p0 is the camera eye and
+// the numerator n . (v0 - eye) was computed for it by rt_prepare_kernel with the same operations.
+template <bool PRIMARY = false>
 __device__ __forceinline__ bool board_hit(const DevScene* S, d3 p0, d3 d, d3* p) {
     const DevTri& T = S->tri[0];
     d3 n = ld3(T.n);
     double nd = dot(n, d);                                  // :648
     if (fabs(nd) < S->eps) return false;                    // :651
     d3 v0 = ld3(T.v0);
-    double num = dot(n, sub(v0, p0));                       // :657 numerator
+    double num = PRIMARY ? S->board_num : dot(n, sub(v0, p0));   // :657 numerator
     // m = num / nd is <= 0 (hence < eps, a miss at :659) when num == 0 or the signs differ.  NaNs fall
     // through to the division and miss there, as in the reference.
     if (num == 0.0 || ((num < 0.0) != (nd < 0.0))) return false;
@@ -243,8 +269,8 @@ __device__ __forceinline__ bool board_hit(const DevScene* S, d3 p0, d3 d, d3* p)
         // den < 0 (host-checked, else thr = +inf): A > thr = |den| 2^-1070 makes A/den negative and nonzero,
         // so s >= 0 fails without dividing; likewise B for t.
         if (A > Tt.thr || B > Tt.thr) continue;
-        double s = A / Tt.den;                              // :673
-        double tt = B / Tt.den;                             // :674
+        double s = div_const(A, Tt.den, Tt.rden, Tt.fast);  // :673
+        double tt = div_const(B, Tt.den, Tt.rden, Tt.fast); // :674
         if (s >= 0 && tt >= 0 && s + tt <= 1) {             // :676
             *p = q;
             return true;
@@ -272,8 +298,8 @@ __device__ __forceinline__ bool tri_hit(const DevTri& T, d3 p0, d3 d, double eps
     double A = T.uv * wv - T.vv * wu;
     double B = T.uv * wu - T.uu * wv;
     if (A > T.thr || B > T.thr) return false;
-    double s = A / T.den;                                   // :673
-    double tt = B / T.den;                                  // :674
+    double s = div_const(A, T.den, T.rden, T.fast);         // :673
+    double tt = div_const(B, T.den, T.rden, T.fast);        // :674
     if (s >= 0 && tt >= 0 && s + tt <= 1) {                 // :676
         *p = q;
         return true;
@@ -396,9 +422,16 @@ __device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const R
     uint32_t pass = 0;
 #pragma unroll
     for (int j = 0; j < kChunk; ++j) pass |= (sphere_reject32(V.sphf[k0 + j], r) ? 0u : 1u) << j;
+#if RT_UNIFORM_SECONDARY
+#pragma unroll
+    for (int j = 0; j < kChunk; ++j) {
+        if (!(pass & (1u << j))) continue;                  // skipped by the wave when no lane needs it
+        const int k = k0 + j;
+#else
     while (pass) {
         const int k = k0 + __builtin_ctz(pass);
         pass &= pass - 1;
+#endif
         d3 q;
         if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) {
             double dist = len_fast(sub(q, r.p0));                // :811-812
@@ -487,7 +520,7 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
     double best = -1.0;
     if (S->has_board) {
         d3 q;
-        if (board_hit(S, r.p0, r.d, &q)) {
+        if (board_hit<true>(S, r.p0, r.d, &q)) {
             kind = 0;
             best = len_fast(sub(q, r.p0));
             *hp = q;
@@ -510,9 +543,16 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
             uD = fmaf(r.uz, f.dz, uD);
             pass |= (fmaf(uD, uD, f.c0) < 0.0f ? 0u : 1u) << j;   // < 0: certain disc < 0
         }
+#if RT_UNIFORM_PRIMARY
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            if (!(pass & (1u << j))) continue;
+            const int k = k0 + j;
+#else
         while (pass) {
             const int k = k0 + __builtin_ctz(pass);
             pass &= pass - 1;
+#endif
             const DevSpherePrim& pp = V.prim[k];
             d3 q;
             if (sphere_hit_dp(ld3(pp.dP), pp.dd, V.sph[k].r2, r.p0, r.u, eps, &q)) {
@@ -709,9 +749,16 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
             t = fmaf(r.uz, f.vz, t);
             pass |= (fabsf(t) < f.c ? 0u : 1u) << j;
         }
+#if RT_UNIFORM_SHADOW
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            if (!(pass & (1u << j))) continue;
+            const int k = k0 + j;
+#else
         while (pass) {
             const int k = k0 + __builtin_ctz(pass);
             pass &= pass - 1;
+#endif
             d3 q;
             if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) return true;
         }
@@ -740,7 +787,7 @@ __device__ __forceinline__ int material_of(const SceneView& V, int kind, d3 p) {
     const DevScene* S = V.S;
     if (kind == 0) {
         d3 q = add(sub(p, ld3(S->coff)), mk(S->half, 0.0, S->half));
-        const double r = rcp_core(S->square);
+        const double r = S->rsquare;                        // rcp_core(square), rt_scene_init_kernel
         int squareSum = (int)div_core(q.x, S->square, r) + (int)div_core(q.z, S->square, r);
         return (squareSum & 1) == 0 ? 0 : 1;
     }

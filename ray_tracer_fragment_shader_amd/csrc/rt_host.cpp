@@ -61,6 +61,12 @@ void set_material(rt_material* m, HP a, HP d, HP s, HP t, double r) {
     m->refraction = r;
 }
 
+// The kernel divides by a triangle's den with a shared reciprocal (rt_device.hpp div_const) only when
+// |den| is in [2^-200, 2^200]: with |A| in [2^-500, 2^500] the IEEE sequence's scale steps are identities.
+int32_t const_quotient_ok(double den) {
+    return std::fabs(den) >= 0x1p-200 && std::fabs(den) <= 0x1p+200 ? 1 : 0;
+}
+
 bool valid_square(const char* sq) { return sq && sq[0] != 0 && sq[1] != 0; }
 
 bool all_zero(const double v[3]) { return v[0] == 0 && v[1] == 0 && v[2] == 0; }
@@ -347,6 +353,7 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
             // Otherwise disable the shortcut.
             T.thr = (den < 0 && std::fabs(den) >= 1024.0) ? std::ldexp(std::fabs(den), -1070)
                                                           : std::numeric_limits<double>::infinity();
+            T.fast = const_quotient_ok(den);
         }
         // The kernel shares the plane step of the two triangles; the reference board always satisfies
         // this (same vertex 0, same normal).  A degenerate board never intersects (:633-637).
@@ -489,6 +496,7 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
             T.vv = vv;
             T.den = den;
             T.thr = (den < 0 && std::fabs(den) >= 1024.0) ? std::ldexp(std::fabs(den), -1070) : inf;
+            T.fast = const_quotient_ok(den);
             T.degenerate = degenerate ? 1.0 : 0.0;
         }
     }

@@ -81,8 +81,10 @@ __device__ __forceinline__ void stage_scene(char* dst, const DevScene* __restric
     for (int k = threadIdx.x; k < (bytes >> 4); k += kThreads) d[k] = s[k];
 }
 
+// floor(clamp(c, 0, 1) * 255 + 0.5) (RGBA8 definition).  fmax/fmin (v_max/v_min_f64) clamp
+// exactly like the comparisons; NaN becomes 0 (the conversion of a NaN is 0 on the device as well).
 __device__ __forceinline__ unsigned char to_u8(double c) {
-    double v = c < 0.0 ? 0.0 : (c > 1.0 ? 1.0 : c);
+    double v = fmin(fmax(c, 0.0), 1.0);
     return (unsigned char)(int)floor(v * 255.0 + 0.5);
 }
 
@@ -124,8 +126,7 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
     const int bx0 = wave * bw, by0 = 0;
     const int cx = bx0 + (lane & 7);               // column inside the tile
     const int cy = lane >> 3;                      // row inside the tile
-    const int tiles_x = (P.width + TW - 1) / TW;
-    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int tx = blockIdx.x, ty = blockIdx.y;     // 2-D grid: tiles_x x tiles_y
     const int i = tx * TW + cx;
     const int lr = ty * kTileH + cy;
     const bool valid = i < P.width && lr < P.local_rows;
@@ -204,7 +205,11 @@ __global__ __launch_bounds__(kThreads) void rt_prepare_kernel(DevScene* __restri
     DevSphereCone* cone = reinterpret_cast<DevSphereCone*>(primf + np);
     const d3 eye = mk(ex, ey, ez);
     const int k = blockIdx.x * kThreads + threadIdx.x;
-    if (k == 0) { g->eye[0] = ex; g->eye[1] = ey; g->eye[2] = ez; }
+    if (k == 0) {
+        g->eye[0] = ex; g->eye[1] = ey; g->eye[2] = ez;
+        // board plane numerator for p0 = eye, as board_hit computes it (:657)
+        g->board_num = dot(ld3(g->tri[0].n), sub(ld3(g->tri[0].v0), eye));
+    }
     if (k >= np) return;
     d3 dP = sub(ld3(sph[k].c), eye);
     double dd = dot(dP, dP);
@@ -239,6 +244,19 @@ __global__ __launch_bounds__(kThreads) void rt_prepare_kernel(DevScene* __restri
         }
     }
     cone[k] = cn;
+}
+
+// Eye-independent reciprocals of the division shortcuts (run by rt_set_scene): rcp_core of the checker
+// square and of every triangle's den, with the compiler's own Newton steps (rt_device.hpp div_core).
+__global__ __launch_bounds__(kThreads) void rt_scene_init_kernel(DevScene* __restrict__ g) {
+    const int k = blockIdx.x * kThreads + threadIdx.x;
+    if (k == 0) g->rsquare = rcp_core(g->square);
+    if (k < 2) g->tri[k].rden = g->tri[k].fast ? rcp_core(g->tri[k].den) : 0.0;
+    const SceneView V = view_of(g, g, g->n_padded, g->n_lights);
+    if (k < g->n_tris) {
+        DevTri* t = const_cast<DevTri*>(V.tri) + k;
+        t->rden = t->fast ? rcp_core(t->den) : 0.0;
+    }
 }
 
 template <int B, bool TRANSP>
@@ -464,6 +482,10 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     RT_HIP(hipMemcpy(c->d_scene, blob.data(), blob.size(), hipMemcpyHostToDevice));
     c->scene_bytes = (int)blob.size();
     const rt::DevScene* h = reinterpret_cast<const rt::DevScene*>(blob.data());
+    hipLaunchKernelGGL(rt_scene_init_kernel, dim3((unsigned)((std::max(h->n_tris, 2) + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, nullptr, c->d_scene);
+    RT_HIP(hipGetLastError());
+    RT_HIP(hipDeviceSynchronize());
     c->lds_bytes = h->lds_bytes;
     c->n_padded = h->n_padded;
     c->n_lights = h->n_lights;
@@ -542,15 +564,16 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     const int tw = big ? kTileW : 8;
     const int tiles_x = (W + tw - 1) / tw;
     const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
-    dim3 grid((unsigned)(tiles_x * tiles_y));
+    if (tiles_y > 65535) return rt_fail(RT_EINVAL, "render: more than 524,280 local rows");
+    dim3 grid((unsigned)tiles_x, (unsigned)tiles_y);
     const size_t lds64 = slot_bytes(depth, c->transparent, 64);
     const size_t lds256 = (c->wg_staging ? 4096 + 6144 + 1024 + 1024 : 0) + slot_bytes(depth, c->transparent);
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     // Primary-ray sphere data for this eye (stream-ordered; only when the eye changes).
     if (!c->eye_valid || memcmp(c->eye, cam->eye, sizeof(c->eye)) != 0) {
-        if (c->n_padded > 0) {
-            dim3 pg((unsigned)((c->n_padded + kThreads - 1) / kThreads));
+        {
+            dim3 pg((unsigned)((std::max(c->n_padded, 1) + kThreads - 1) / kThreads));
             hipLaunchKernelGGL(rt_prepare_kernel, pg, dim3(kThreads), 0, st, c->d_scene, cam->eye[0], cam->eye[1],
                                cam->eye[2]);
             e = hipGetLastError();

@@ -34,6 +34,9 @@ struct alignas(16) DevTri {            // Triangle after its ctor (:406-433), ve
     double uv, uu, vv, den;
     double thr;                        // |den| * 2^-1070: A > thr  =>  A/den < 0 and nonzero
     double degenerate;                 // 1.0: this triangle never intersects (:633-637)
+    double rden;                       // rcp_core(den), computed on the device (rt_scene_init_kernel)
+    int32_t fast;                      // 1: |den| in [2^-200, 2^200], quotients A/den may use rden
+    int32_t pad;
 };
 
 struct alignas(16) DevMat {            // the colour terms rayTraceRay reads (:1224-1226) and its continuation
@@ -96,7 +99,9 @@ struct alignas(16) DevScene {
     double coff[3];                    // checker offset = positionOffset of CheckerBoard (:1101)
     double half;                       // BOARD_HALF_SIZE
     double square;                     // SQUARE_EDGE_SIZE
-    double eye[3];                     // camera the *Prim arrays were computed for
+    double rsquare;                    // rcp_core(square), computed on the device (rt_scene_init_kernel)
+    double board_num;                  // n . (v0 - eye) of the board plane for the camera `eye` (per eye)
+    double eye[3];                     // camera the *Prim arrays and board_num were computed for
     int32_t bound_on;                  // g_scene radius > 0
     int32_t has_board;
     int32_t n_spheres;                 // real spheres

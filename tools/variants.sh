@@ -5,14 +5,14 @@ set -eu
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 SRC=$ROOT/ray_tracer_fragment_shader_amd/csrc
 LIB=$ROOT/ray_tracer_fragment_shader_amd/lib
-make -C "$SRC" -s ../lib/rt_host.o
+make -C "$SRC" -s ../lib/rt_host.o ../lib/rt_screen.o
 pids=()
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
   d=$ROOT/tools/_var/$name; mkdir -p "$d"
   ( cd "$SRC" && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function \
       --offload-arch=gfx950 $flags -c rt_kernel.hip -o "$d/rt_kernel.o" && \
-    /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$d/librt_amd.so" "$d/rt_kernel.o" "$LIB/rt_host.o" && \
+    /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$d/librt_amd.so" "$d/rt_kernel.o" "$LIB/rt_host.o" "$LIB/rt_screen.o" && \
     rm "$d/rt_kernel.o" && echo "built $name" ) &
   pids+=($!)
 done
