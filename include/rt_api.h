@@ -20,6 +20,8 @@
  *    with RT_EHIP.
  *  - One rt_ctx per (thread, device).  A context owns the device copy of the scene; rt_render_dev is
  *    asynchronous on the caller's stream and does not allocate, so it may be captured in a hipGraph.
+ *    A context's renders must be stream-ordered (one stream at a time): a render may update the
+ *    context's per-camera data (sphere data for a new eye, the tile-row dispatch order).
  */
 #ifndef RT_API_H
 #define RT_API_H

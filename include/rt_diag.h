@@ -21,6 +21,13 @@ extern "C" {
  * Asynchronous on `stream`.  RT_EINVAL for an unknown op or null buffers. */
 int rt_probe_math_dev(int op, const double* in, int n, double* out, void* stream);
 
+/* Tile-row dispatch order of later rt_render_dev calls of this context: mode 0 (default) adaptive — the
+ * first render of a new (scene, camera, size, row plan, depth) times its 8-row tile rows and later
+ * renders dispatch them longest first; mode 1 bottom-to-top.  Images are identical either way (every
+ * tile is traced once, by the same code).  RT_EINVAL for another mode. */
+typedef struct rt_ctx rt_ctx;
+int rt_diag_tile_order(rt_ctx* ctx, int mode);
+
 #ifdef __cplusplus
 }
 #endif

@@ -126,8 +126,10 @@ SIGNATURES = {
                                  c_void_p, c_void_p, c_void_p, _P(ctypes.c_uint64)]),
     # include/rt_diag.h
     "rt_probe_math_dev": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "rt_diag_tile_order": (c_int, [c_void_p, c_int]),
 }
 
+_DIAG = {"rt_diag_tile_order"}
 _lib = None
 
 
@@ -140,6 +142,8 @@ def lib() -> ctypes.CDLL:
                                f"g.build()'` (make -C ray_tracer_fragment_shader_amd/csrc)")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if name in _DIAG and not hasattr(L, name):
+                continue                     # diagnostics of rt_diag.h (older builds in A/B timing tools)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

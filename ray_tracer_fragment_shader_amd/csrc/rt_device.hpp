@@ -39,6 +39,9 @@
 // 1: the exact tests of a filter batch visit its spheres in a loop the whole wave runs (record index
 // wave-uniform: scalar loads, SGPR operands; lanes whose filter rejected a sphere are masked off);
 // 0: each lane walks its own surviving spheres (per-lane index: vector loads).
+#ifndef RT_FAST_FALLBACK
+#define RT_FAST_FALLBACK 0
+#endif
 #ifndef RT_UNIFORM_PRIMARY
 #define RT_UNIFORM_PRIMARY 1
 #endif
@@ -99,7 +102,13 @@ __device__ __forceinline__ double sqrt_core(double x) {
     return fma(d, h, g);
 }
 
-__device__ __forceinline__ bool sqrt_fast_ok(double x) { return x >= 0x1p-700 && x <= 0x1p+700; }
+// The range checks are evaluated without short-circuits (& and | on bools: compares combined in SGPR
+// masks, no exec-mask branches), and the rare fallback is one wave-uniform branch taken only when some lane
+// needs it (RT_FAST_FALLBACK).
+__device__ __forceinline__ bool sqrt_fast_ok(double x) { return (x >= 0x1p-700) & (x <= 0x1p+700); }
+
+// True when some active lane of the wave has `bad` set (the fast paths' fallback branch).
+__device__ __forceinline__ bool any_lane(bool bad) { return __ballot(bad) != 0; }
 
 __device__ __forceinline__ double rcp_core(double b) {
     double r = __builtin_amdgcn_rcp(b);
@@ -115,7 +124,7 @@ __device__ __forceinline__ double div_core(double a, double b, double r) {
     return fma(e, r, q);
 }
 
-__device__ __forceinline__ bool num_fast_ok(double a) { return a == 0.0 || fabs(a) >= 0x1p-500; }
+__device__ __forceinline__ bool num_fast_ok(double a) { return (a == 0.0) | (fabs(a) >= 0x1p-500); }
 
 // a / b for a constant b with r = rcp_core(b) precomputed on the device (rt_scene_init_kernel).  `fast`
 // (host): |b| in [2^-200, 2^200]; then for |a| in [2^-500, 2^500] the quotient's exponent is within
@@ -123,13 +132,30 @@ __device__ __forceinline__ bool num_fast_ok(double a) { return a == 0.0 || fabs(
 // and div_core is the IEEE quotient bit for bit (fast paths above); other operands (zero, tiny, huge,
 // NaN) take the compiler's division.
 __device__ __forceinline__ double div_const(double a, double b, double r, int32_t fast) {
+#if RT_FAST_FALLBACK
+    const double aa = fabs(a);
+    const bool ok = (fast != 0) & (aa >= 0x1p-500) & (aa <= 0x1p+500);
+    double q = div_core(a, b, r);
+    if (any_lane(!ok)) q = ok ? q : a / b;
+    return q;
+#else
     const double aa = fabs(a);
     if (fast && aa >= 0x1p-500 && aa <= 0x1p+500) return div_core(a, b, r);
     return a / b;
+#endif
 }
 
 // sqrt(x), bit-identical, with the fast sequence when it applies.
-__device__ __forceinline__ double sqrt_fast(double x) { return sqrt_fast_ok(x) ? sqrt_core(x) : sqrt(x); }
+__device__ __forceinline__ double sqrt_fast(double x) {
+#if RT_FAST_FALLBACK
+    const bool ok = sqrt_fast_ok(x);
+    double y = sqrt_core(x);
+    if (any_lane(!ok)) y = ok ? y : sqrt(x);
+    return y;
+#else
+    return sqrt_fast_ok(x) ? sqrt_core(x) : sqrt(x);
+#endif
+}
 
 // |a| (= len(a), :174).
 __device__ __forceinline__ double len_fast(d3 a) { return sqrt_fast(a.x * a.x + a.y * a.y + a.z * a.z); }
@@ -137,6 +163,21 @@ __device__ __forceinline__ double len_fast(d3 a) { return sqrt_fast(a.x * a.x + 
 // u = a / |a| component-wise (= divs(a, len(a)), :174-175, Line::direction :258-263); *l = |a|.
 __device__ __forceinline__ d3 unit(d3 a, double* l) {
     double s = a.x * a.x + a.y * a.y + a.z * a.z;
+#if RT_FAST_FALLBACK
+    const bool ok = sqrt_fast_ok(s) & num_fast_ok(a.x) & num_fast_ok(a.y) & num_fast_ok(a.z);
+    double L = sqrt_core(s);
+    double r = rcp_core(L);
+    d3 u = mk(copysign(div_core(a.x, L, r), a.x), copysign(div_core(a.y, L, r), a.y),
+              copysign(div_core(a.z, L, r), a.z));
+    if (any_lane(!ok)) {
+        if (!ok) {
+            L = sqrt(s);
+            u = divs(a, L);
+        }
+    }
+    *l = L;
+    return u;
+#else
     if (sqrt_fast_ok(s) && num_fast_ok(a.x) && num_fast_ok(a.y) && num_fast_ok(a.z)) {
         double L = sqrt_core(s);
         double r = rcp_core(L);
@@ -147,6 +188,7 @@ __device__ __forceinline__ d3 unit(d3 a, double* l) {
     double L = sqrt(s);
     *l = L;
     return divs(a, L);
+#endif
 }
 
 __device__ __forceinline__ d3 unit(d3 a) {

@@ -33,6 +33,14 @@
 
 using namespace rt;
 
+#ifndef RT_WAVE_TRACE
+#define RT_WAVE_TRACE 0
+#endif
+// __launch_bounds__ minimum waves per EU of the depth <= 3 render kernels (5: <= 96 VGPRs).
+#ifndef RT_MINW
+#define RT_MINW 5
+#endif
+
 namespace {
 
 constexpr int kTileW = 32;   // workgroup tile: 32 columns ...
@@ -64,6 +72,8 @@ struct RenderParams {
     int32_t wg_staging;                        // 1: stage the 32 x 8 tile in LDS behind a workgroup barrier
     float look32[3], right32[3], upp32[3], eye32[3], pitch32;   // FP32 camera for primary_cone_mask
     float cone_slack;                          // its error bound (render_params)
+    const int32_t* tile_rows;                  // dispatch order of tile rows (nullptr: bottom to top)
+    uint32_t* row_cost;                        // calibration render: per tile row, sum of wave times (100 MHz)
 };
 
 // Image row (within its frame) of local row lr; local rows are frame-major (rt_rows.frames).
@@ -88,6 +98,11 @@ __device__ __forceinline__ unsigned char to_u8(double c) {
     return (unsigned char)(int)floor(v * 255.0 + 0.5);
 }
 
+#if RT_WAVE_TRACE
+// Diagnostic build only (tools/wave_trace.py): per workgroup {start, end} shader-clock stamps and HW_ID.
+__device__ uint64_t* g_wtrace = nullptr;
+#endif
+
 template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads>
 __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
                                                              RenderParams P, float4* __restrict__ out32,
@@ -96,6 +111,10 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
                                                              uint32_t* __restrict__ outrc) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
+#if RT_WAVE_TRACE
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    const uint64_t t_cal = P.row_cost ? __builtin_amdgcn_s_memrealtime() : 0;
     // LDS: [header | DevSphere[np] | DevSpherePrim[np]] (LDS = 1), the per-level colour slots of trace()
     // (slot_bytes), then the output staging tile (12 KB, RT_WG_STAGING only).
     // The scene record is broadcast into LDS once per workgroup; the FP32 filter images stay in global
@@ -126,7 +145,8 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
     const int bx0 = wave * bw, by0 = 0;
     const int cx = bx0 + (lane & 7);               // column inside the tile
     const int cy = lane >> 3;                      // row inside the tile
-    const int tx = blockIdx.x, ty = blockIdx.y;     // 2-D grid: tiles_x x tiles_y
+    const int tx = blockIdx.x;                      // 2-D grid: tiles_x x tiles_y
+    const int ty = P.tile_rows ? P.tile_rows[blockIdx.y] : (int)blockIdx.y;
     const int i = tx * TW + cx;
     const int lr = ty * kTileH + cy;
     const bool valid = i < P.width && lr < P.local_rows;
@@ -166,6 +186,17 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
             if (outrc) outrc[k] = seg | (sh << 16);
             if (out8) out8[k] = make_uchar4(to_u8(col.x), to_u8(col.y), to_u8(col.z), 255);
         }
+        if (P.row_cost && tid == 0)
+            atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
+#if RT_WAVE_TRACE
+        if (g_wtrace && tid == 0) {
+            const size_t w = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+            g_wtrace[3 * w] = t_start;
+            g_wtrace[3 * w + 1] = __builtin_amdgcn_s_memrealtime();
+            g_wtrace[3 * w + 2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                                  ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
+        }
+#endif
         return;
     }
     // Stage through LDS, then store whole tile rows.
@@ -188,6 +219,35 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
         if (outrc) outrc[k] = strc[tid];
         if (out8) out8[k] = st8[tid];
     }
+    if (P.row_cost && tid == 0) atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
+}
+
+// Tile-row dispatch order from a calibration render's per-row costs: rows by decreasing cost (ties by
+// index), so the longest rows are dispatched first and the cheap ones fill the tail (longest-processing-
+// time-first list scheduling).  One workgroup, bitonic sort of (~cost, row) keys in LDS; n <= kOrderMax.
+constexpr int kOrderMax = 8192;
+__global__ __launch_bounds__(1024) void rt_order_kernel(const uint32_t* __restrict__ cost, int n,
+                                                        int32_t* __restrict__ order) {
+    __shared__ uint64_t key[kOrderMax];
+    int m = 1;
+    while (m < n) m <<= 1;
+    for (int k = threadIdx.x; k < m; k += blockDim.x)
+        key[k] = k < n ? ((uint64_t)(~cost[k]) << 32) | (uint32_t)k : ~0ull;
+    __syncthreads();
+    for (int size = 2; size <= m; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int k = threadIdx.x; k < m; k += blockDim.x) {
+                const int o = k ^ stride;
+                if (o > k) {
+                    const bool up = (k & size) == 0;
+                    const uint64_t a = key[k], b = key[o];
+                    if ((a > b) == up) { key[k] = b; key[o] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int k = threadIdx.x; k < n; k += blockDim.x) order[k] = (int32_t)(key[k] & 0xffffffffu);
 }
 
 // Per-eye primary-ray sphere data (run by rt_render_dev when the camera eye changes): deltaP = C - eye
@@ -413,6 +473,16 @@ struct rt_ctx {
                                                // despite small spills: tools/ab.py); RT_MIN_WAVES=0 disables
     int use_lds = 0;                           // RT_SCENE_IN_LDS=1: header + exact records in LDS (A/B: tools/ab.py)
     int wg_staging = 0;                        // RT_WG_STAGING=1: LDS-staged 32-pixel row stores (A/B)
+    // Adaptive tile-row order (rt_order_kernel): the first render of a new (scene, camera, size, rows,
+    // depth) is a calibration render that also times its tile rows; later renders dispatch the rows by
+    // decreasing time.  order_mode (rt_diag_tile_order): 0 adaptive, 1 bottom-to-top.
+    int32_t* d_tile_rows = nullptr;
+    uint32_t* d_row_cost = nullptr;
+    int n_tile_rows = 0;                       // capacity of both (kOrderMax, allocated by rt_ctx_create)
+    bool order_valid = false;
+    std::vector<unsigned char> order_key;
+    int order_mode = 0;
+    uint64_t scene_gen = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -421,6 +491,12 @@ struct rt_ctx {
         hipError_t e_ = (call);                                                                       \
         if (e_ != hipSuccess) return rt_fail(RT_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
     } while (0)
+
+#if RT_WAVE_TRACE
+extern "C" int rt_debug_wave_trace(void* dev_buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace), &dev_buf, sizeof(dev_buf)) == hipSuccess ? RT_OK : RT_EHIP;
+}
+#endif
 
 extern "C" int rt_device_count(int* count) {
     if (!count) return rt_fail(RT_EINVAL, "rt_device_count: null pointer");
@@ -447,6 +523,12 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_SCENE_IN_LDS")) c->use_lds = atoi(e) != 0;
     if (const char* e = getenv("RT_MIN_WAVES")) c->min_waves = atoi(e);
     if (const char* e = getenv("RT_WG_STAGING")) c->wg_staging = atoi(e) != 0;
+    if (hipMalloc(&c->d_tile_rows, sizeof(int32_t) * kOrderMax) != hipSuccess ||
+        hipMalloc(&c->d_row_cost, sizeof(uint32_t) * kOrderMax) != hipSuccess) {
+        rt_ctx_destroy(c);
+        return rt_fail(RT_ENOMEM, "rt_ctx_create: hipMalloc of the tile-row order failed");
+    }
+    c->n_tile_rows = kOrderMax;
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         delete c;
         return rt_fail(RT_EHIP, "rt_ctx_create: hipEventCreate failed");
@@ -459,6 +541,8 @@ extern "C" int rt_ctx_destroy(rt_ctx* c) {
     if (!c) return RT_OK;
     (void)hipSetDevice(c->device);
     if (c->d_scene) (void)hipFree(c->d_scene);
+    if (c->d_tile_rows) (void)hipFree(c->d_tile_rows);
+    if (c->d_row_cost) (void)hipFree(c->d_row_cost);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c;
@@ -492,6 +576,7 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     c->transparent = h->transparent != 0 || h->n_meshes > 0;   // FULL kernel variants
     c->eye_valid = false;
     c->scene_set = true;
+    ++c->scene_gen;
     return RT_OK;
 }
 
@@ -565,6 +650,26 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     const int tiles_x = (W + tw - 1) / tw;
     const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
     if (tiles_y > 65535) return rt_fail(RT_EINVAL, "render: more than 524,280 local rows");
+    hipStream_t st0 = (hipStream_t)stream;
+    if (c->order_mode == 0 && tiles_y <= c->n_tile_rows) {
+        // Key of the frame's work: camera, size, row plan, depth and scene generation.
+        std::vector<unsigned char> key(sizeof(rt_camera) + 5 * sizeof(int) + sizeof(rt_rows) + sizeof(uint64_t), 0);
+        unsigned char* kp = key.data();
+        memcpy(kp, cam, sizeof(rt_camera)); kp += sizeof(rt_camera);
+        const int ints[5] = {W, H, depth, tiles_x, tiles_y};
+        memcpy(kp, ints, sizeof(ints)); kp += sizeof(ints);
+        if (rows) memcpy(kp, rows, sizeof(rt_rows));
+        kp += sizeof(rt_rows);
+        memcpy(kp, &c->scene_gen, sizeof(uint64_t));
+        if (c->order_valid && key == c->order_key) {
+            P.tile_rows = c->d_tile_rows;
+        } else {
+            RT_HIP(hipMemsetAsync(c->d_row_cost, 0, sizeof(uint32_t) * tiles_y, st0));
+            P.row_cost = c->d_row_cost;                 // calibration render (identity order)
+            c->order_key = key;
+            c->order_valid = true;
+        }
+    }
     dim3 grid((unsigned)tiles_x, (unsigned)tiles_y);
     const size_t lds64 = slot_bytes(depth, c->transparent, 64);
     const size_t lds256 = (c->wg_staging ? 4096 + 6144 + 1024 + 1024 : 0) + slot_bytes(depth, c->transparent);
@@ -591,15 +696,20 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
         e = launch_render_lds<1, 1, false, false, kThreads>(depth, grid, c->lds_bytes + lds256, st, c->d_scene, P,
                                                              o32, o8, rgb64f, raycount);
     else if (c->wg_staging)
-        e = (mw5 ? launch_render_lds<0, 5, false, false, kThreads> : launch_render_lds<0, 1, false, false, kThreads>)(
+        e = (mw5 ? launch_render_lds<0, RT_MINW, false, false, kThreads> : launch_render_lds<0, 1, false, false, kThreads>)(
                 depth, grid, lds256, st, c->d_scene, P, o32, o8, rgb64f, raycount);
     else {
         // >= kConeMin spheres: the wave-culling variant (secondary and shadow rays, rt_device.hpp CULL).
-        auto launch = cull ? (mw5 ? launch_render_lds<0, 5, false, true, 64> : launch_render_lds<0, 1, false, true, 64>)
-                           : (mw5 ? launch_render_lds<0, 5, false, false, 64> : launch_render_lds<0, 1, false, false, 64>);
+        auto launch = cull ? (mw5 ? launch_render_lds<0, RT_MINW, false, true, 64> : launch_render_lds<0, 1, false, true, 64>)
+                           : (mw5 ? launch_render_lds<0, RT_MINW, false, false, 64> : launch_render_lds<0, 1, false, false, 64>);
         e = launch(depth, grid, lds64, st, c->d_scene, P, o32, o8, rgb64f, raycount);
     }
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_kernel launch: ") + hipGetErrorString(e));
+    if (P.row_cost) {
+        hipLaunchKernelGGL(rt_order_kernel, dim3(1), dim3(1024), 0, st, c->d_row_cost, tiles_y, c->d_tile_rows);
+        e = hipGetLastError();
+        if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_order_kernel: ") + hipGetErrorString(e));
+    }
     return RT_OK;
 }
 
@@ -701,6 +811,15 @@ extern "C" int rt_unshuffle_dev(const void* gathered, void* image, int W, int H,
                        (const uint32_t*)gathered, (uint32_t*)image, row_words, H, band_height, n_ranks, slab_rows);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_unshuffle_kernel: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+// Diagnostics (include/rt_diag.h): tile-row dispatch order of later renders: 0 adaptive (default), 1
+// bottom-to-top.
+extern "C" int rt_diag_tile_order(rt_ctx* c, int mode) {
+    if (!c || (mode != 0 && mode != 1)) return rt_fail(RT_EINVAL, "rt_diag_tile_order: bad args");
+    c->order_mode = mode;
+    c->order_valid = false;
     return RT_OK;
 }
 

@@ -538,3 +538,32 @@ def test_checker_division_fast_path(tr):
     assert _same_bits(o[regular, 1], ieee[regular]).all()
     board = np.abs(a) <= 1e4
     assert np.array_equal(np.trunc(o[board, 1]), np.trunc(ieee[board]))
+
+
+@pytest.mark.parametrize("name,W,H,rows", [("c2", 480, 270, None), ("c5", 640, 360, None),
+                                           ("c3", 400, 300, (4, 3, 1, 2))])
+def test_tile_order_adaptive(tr, name, W, H, rows):
+    """The adaptive tile-row order (a calibration render times its tile rows, later renders dispatch them
+    longest first, rt_order_kernel) only reorders work: every render is bit-identical to the bottom-to-top
+    order and to the oracle."""
+    cfg = scenes.CONFIGS[name]
+    sc, cam = cfg.scene(), cfg.camera(W, H)
+    rr = abi.rt_rows(*rows) if rows else None
+    lib = abi.lib()
+    try:
+        abi.check(lib.rt_diag_tile_order(tr._ctx, 1), "rt_diag_tile_order")
+        base, base_rc = _render64(tr, sc, cam, W, H, cfg.depth, rows=rr)
+        abi.check(lib.rt_diag_tile_order(tr._ctx, 0), "rt_diag_tile_order")
+        tr.set_scene(sc)
+        for k in range(3):                       # calibration render, then two ordered renders
+            b = tr.render(cam, W, H, cfg.depth, rows=rr, rgba32f=False, rgb64f=True, raycount=True)
+            torch.cuda.synchronize()
+            assert np.array_equal(b["rgb64f"].cpu().numpy(), base, equal_nan=True), f"render {k} differs"
+            assert np.array_equal(b["raycount"].cpu().numpy().view(np.uint32), base_rc)
+    finally:
+        lib.rt_diag_tile_order(tr._ctx, 0)
+    if rows is None and name != "c5":
+        want, _ = po.render(sc.to_abi(), cam, W, H, cfg.depth)
+        _assert_parity(base, want)
+    with pytest.raises(abi.RtError):
+        abi.check(lib.rt_diag_tile_order(tr._ctx, 7), "rt_diag_tile_order")

@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-from ray_tracer_fragment_shader_amd import scenes  # noqa: E402
+from ray_tracer_fragment_shader_amd import abi, scenes  # noqa: E402
 from ray_tracer_fragment_shader_amd.tracer import Tracer  # noqa: E402
 
 
@@ -22,6 +22,7 @@ def main():
     cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c1", "c2", "c3", "c5"]
     modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["base", "RT_SCENE_IN_LDS=1"]
     rounds = int(os.environ.get("ROUNDS", "5"))
+    order = os.environ.get("TILE_ORDER")          # 0 adaptive / 1 bottom-to-top (rt_diag_tile_order)
     reps = int(os.environ.get("REPS", "10"))
     tracers = {}
     for m in modes:
@@ -31,6 +32,8 @@ def main():
                 k, v = kv.split("=")
                 os.environ[k] = v
         tracers[m] = Tracer(0)
+        if order is not None and hasattr(abi.lib(), "rt_diag_tile_order"):
+            abi.check(abi.lib().rt_diag_tile_order(tracers[m]._ctx, int(order)), "rt_diag_tile_order")
         os.environ.clear()
         os.environ.update(saved)
     res = {(c, m): [] for c in cfgs for m in modes}

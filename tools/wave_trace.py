@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Per-wave timeline of one rt_render_kernel launch (diagnostic; needs the RT_WAVE_TRACE=1 build (copied over lib/librt_amd.so) from
+tools/variants.sh, e.g. `bash tools/variants.sh trace=-DRT_WAVE_TRACE=1`).
+Reports wave durations, concurrent waves over time (per XCD and total) and the tail.
+usage: wave_trace.py [config]"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from ray_tracer_fragment_shader_amd import abi, scenes  # noqa: E402
+from ray_tracer_fragment_shader_amd.tracer import Tracer  # noqa: E402
+
+
+def main():
+    name = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    cfg = scenes.CONFIGS[name]
+    W, H = cfg.width, cfg.height
+    t = Tracer(0)
+    t.set_scene(cfg.scene())
+    bufs = t.alloc(W, H, rgba32f=True, rgba8=True)
+    nwg = ((W + 7) // 8) * ((H + 7) // 8)
+    tr = torch.zeros(nwg * 3, dtype=torch.int64, device="cuda")
+    lib = abi.lib()
+    lib.rt_debug_wave_trace.argtypes = [ctypes.c_void_p]
+    for _ in range(3):
+        t.render_into(cfg.camera(), W, H, cfg.depth, bufs)
+    torch.cuda.synchronize()
+    assert lib.rt_debug_wave_trace(ctypes.c_void_p(tr.data_ptr())) == 0
+    t.render_into(cfg.camera(), W, H, cfg.depth, bufs)
+    torch.cuda.synchronize()
+    a = tr.cpu().numpy().reshape(nwg, 3)
+    st, en, hw = a[:, 0], a[:, 1], a[:, 2]
+    t0 = st.min()
+    st, en = (st - t0) * 10.0 / 1000.0, (en - t0) * 10.0 / 1000.0       # 100 MHz ticks -> us
+    dur = en - st
+    hwid = hw & 0xFFFFFFFF
+    xcc = (hw >> 32) & 0xF
+    cu = (hwid >> 8) & 0xF
+    se = (hwid >> 13) & 0x7
+    simd = (hwid >> 4) & 0x3
+    grid = np.linspace(0, en.max(), 41)
+    conc = [int(((st <= x) & (en > x)).sum()) for x in grid]
+    out = {
+        "config": name, "waves": int(nwg), "span_us": round(float(en.max()), 2),
+        "dur_us": {q: round(float(np.percentile(dur, q)), 2) for q in (5, 25, 50, 75, 95, 99, 100)},
+        "mean_dur_us": round(float(dur.mean()), 3),
+        "sum_dur_us_per_slot": round(float(dur.sum()) / (256 * 4 * 5), 2),
+        "last_start_us": round(float(st.max()), 2),
+        "p99_end_us": round(float(np.percentile(en, 99)), 2),
+        "concurrency_over_time": conc,
+        "xcc_counts": np.bincount(xcc, minlength=8).tolist(),
+        "xcc_last_end_us": [round(float(en[xcc == k].max()), 2) if (xcc == k).any() else None for k in range(8)],
+        "distinct_cu": int(len(set(zip(xcc.tolist(), se.tolist(), cu.tolist())))),
+        "simd_counts": np.bincount(simd, minlength=4).tolist(),
+    }
+    # duration by image row band (bottom = board rows)
+    rows = (H + 7) // 8
+    d2 = dur.reshape(rows, (W + 7) // 8)
+    out["dur_by_tile_row_us"] = [round(float(x), 2) for x in d2.mean(axis=1)[:: max(1, rows // 16)]]
+    print(json.dumps(out))
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    np.savez(os.path.join(ROOT, "gpurun_out", f"wave_trace_{name}.npz"), start_us=st, end_us=en, hw=hw,
+             tiles_x=(W + 7) // 8, tiles_y=(H + 7) // 8)
+
+
+if __name__ == "__main__":
+    main()
