@@ -523,6 +523,7 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_SCENE_IN_LDS")) c->use_lds = atoi(e) != 0;
     if (const char* e = getenv("RT_MIN_WAVES")) c->min_waves = atoi(e);
     if (const char* e = getenv("RT_WG_STAGING")) c->wg_staging = atoi(e) != 0;
+    if (const char* e = getenv("RT_TILE_ORDER")) c->order_mode = atoi(e) == 1 ? 1 : 0;   // 1: bottom-to-top (A/B)
     if (hipMalloc(&c->d_tile_rows, sizeof(int32_t) * kOrderMax) != hipSuccess ||
         hipMalloc(&c->d_row_cost, sizeof(uint32_t) * kOrderMax) != hipSuccess) {
         rt_ctx_destroy(c);
@@ -652,11 +653,14 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     if (tiles_y > 65535) return rt_fail(RT_EINVAL, "render: more than 524,280 local rows");
     hipStream_t st0 = (hipStream_t)stream;
     if (c->order_mode == 0 && tiles_y <= c->n_tile_rows) {
-        // Key of the frame's work: camera, size, row plan, depth and scene generation.
-        std::vector<unsigned char> key(sizeof(rt_camera) + 5 * sizeof(int) + sizeof(rt_rows) + sizeof(uint64_t), 0);
+        // Key of the frame's work: camera, size, outputs, row plan, depth and scene generation.
+        std::vector<unsigned char> key(sizeof(rt_camera) + 6 * sizeof(int) + sizeof(rt_rows) + sizeof(uint64_t), 0);
         unsigned char* kp = key.data();
         memcpy(kp, cam, sizeof(rt_camera)); kp += sizeof(rt_camera);
-        const int ints[5] = {W, H, depth, tiles_x, tiles_y};
+        // which outputs are written changes the rows' relative cost (an RGB64F parity render writes
+        // 24 B per pixel): each output set gets its own calibration
+        const int outs = (rgba32f ? 1 : 0) | (rgba8 ? 2 : 0) | (rgb64f ? 4 : 0) | (raycount ? 8 : 0);
+        const int ints[6] = {W, H, depth, tiles_x, tiles_y, outs};
         memcpy(kp, ints, sizeof(ints)); kp += sizeof(ints);
         if (rows) memcpy(kp, rows, sizeof(rt_rows));
         kp += sizeof(rt_rows);
