@@ -15,9 +15,12 @@ timeout -k 10 300 python bench.py --steps ${STEPS:-30} --warmup 5 > "$OUT/bench.
 cat "$OUT/bench.json"
 if [ "${PROFILE:-1}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp
+  # the kernel-only bench (no parity render): its 100 timed dispatches dominate the stats; the first
+  # dispatch of the view is the tile-order calibration render (rt_order_kernel follows it once)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-      python3 "$ROOT/bench.py" --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
+      python3 "$ROOT/bench.py" --steps 100 --warmup 5 --no-cpu-baseline --profile-kernel-only > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
       || { echo "rocprof failed"; tail -20 "$OUT/prof.err"; exit 4; }
   find "$OUT/prof" -name "*kernel_stats.csv" -exec cat {} \;
+  cd "$ROOT" && python3 tools/kernel_gaps.py "$OUT/prof" | tee "$OUT/prof_dispatches.json"
 fi
 exit $rc
