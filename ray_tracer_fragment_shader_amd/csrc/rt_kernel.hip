@@ -74,7 +74,10 @@ struct RenderParams {
     float cone_slack;                          // its error bound (render_params)
     const int32_t* tile_rows;                  // dispatch order of tile rows (nullptr: bottom to top)
     uint32_t* row_cost;                        // calibration render: per tile row, sum of wave times (100 MHz)
+    int32_t tile_rows_n;                       // tile rows of this launch
 };
+
+constexpr int kGridY = 32768;                  // grid.y per grid.z slice
 
 // Image row (within its frame) of local row lr; local rows are frame-major (rt_rows.frames).
 __device__ __forceinline__ int global_row_of(const RenderParams& P, int lr) {
@@ -146,7 +149,9 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
     const int cx = bx0 + (lane & 7);               // column inside the tile
     const int cy = lane >> 3;                      // row inside the tile
     const int tx = blockIdx.x;                      // 2-D grid: tiles_x x tiles_y
-    const int ty = P.tile_rows ? P.tile_rows[blockIdx.y] : (int)blockIdx.y;
+    const int gy = (int)(blockIdx.z * kGridY + blockIdx.y);    // tile rows beyond kGridY go to grid.z
+    const int ty = P.tile_rows ? P.tile_rows[gy] : gy;
+    if (ty >= P.tile_rows_n) return;                            // padding of the last grid.z slice
     const int i = tx * TW + cx;
     const int lr = ty * kTileH + cy;
     const bool valid = i < P.width && lr < P.local_rows;
@@ -650,7 +655,7 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     const int tw = big ? kTileW : 8;
     const int tiles_x = (W + tw - 1) / tw;
     const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
-    if (tiles_y > 65535) return rt_fail(RT_EINVAL, "render: more than 524,280 local rows");
+    P.tile_rows_n = tiles_y;
     hipStream_t st0 = (hipStream_t)stream;
     if (c->order_mode == 0 && tiles_y <= c->n_tile_rows) {
         // Key of the frame's work: camera, size, outputs, row plan, depth and scene generation.
@@ -674,7 +679,7 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
             c->order_valid = true;
         }
     }
-    dim3 grid((unsigned)tiles_x, (unsigned)tiles_y);
+    dim3 grid((unsigned)tiles_x, (unsigned)std::min(tiles_y, kGridY), (unsigned)((tiles_y + kGridY - 1) / kGridY));
     const size_t lds64 = slot_bytes(depth, c->transparent, 64);
     const size_t lds256 = (c->wg_staging ? 4096 + 6144 + 1024 + 1024 : 0) + slot_bytes(depth, c->transparent);
     hipStream_t st = (hipStream_t)stream;

@@ -567,3 +567,14 @@ def test_tile_order_adaptive(tr, name, W, H, rows):
         _assert_parity(base, want)
     with pytest.raises(abi.RtError):
         abi.check(lib.rt_diag_tile_order(tr._ctx, 7), "rt_diag_tile_order")
+
+
+def test_tall_frame_grid_slices(tr):
+    """More than 32,768 tile rows: the launch splits its rows over grid.z slices (rt_render_dev)."""
+    cfg = scenes.CONFIGS["c1"]
+    W, H = 2, 8 * 32768 + 20
+    sc, cam = cfg.scene(), cfg.camera(W, H)
+    rgb, rc = _render64(tr, sc, cam, W, H, 1)
+    want, want_rc = po.render(sc.to_abi(), cam, W, H, 1)
+    _assert_parity(rgb, want)
+    assert np.array_equal(rc, want_rc)
