@@ -18,7 +18,10 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <deque>
@@ -160,18 +163,22 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     const V3 up = normalize(cross(right, lookDirection));            // :1276-1277
     V3 walk = (lookAt + (double)cam->bottom_x * right) + (double)cam->bottom_y * up;   // :1279
 
-    // Device and pinned host staging for one chunk.
+    // A chunk's ray ends and colours live in mapped, coherent pinned host memory that the trace kernel
+    // reads and writes directly: a round trip is one launch and one synchronisation, no copies.
     const int kMaxRays = 1 << 16, kMaxPix = 4096;
-    DevBuf d_start, d_end, d_rgb;
+    DevBuf d_start;
     HostBuf h_end, h_rgb;
+    void* d_end = nullptr;
+    void* d_rgb = nullptr;
     Stream st;
     const size_t ray_bytes = (size_t)kMaxRays * 3 * sizeof(double);
+    const unsigned mapped = hipHostMallocMapped | hipHostMallocCoherent;
     hipError_t e = hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&d_start.p, ray_bytes);
-    if (e == hipSuccess) e = hipMalloc(&d_end.p, ray_bytes);
-    if (e == hipSuccess) e = hipMalloc(&d_rgb.p, ray_bytes);
-    if (e == hipSuccess) e = hipHostMalloc(&h_end.p, ray_bytes, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc(&h_rgb.p, ray_bytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc(&h_end.p, ray_bytes, mapped);
+    if (e == hipSuccess) e = hipHostMalloc(&h_rgb.p, ray_bytes, mapped);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&d_end, h_end.p, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&d_rgb, h_rgb.p, 0);
     if (e != hipSuccess) return rt_fail(RT_ENOMEM, std::string("rt_render_screen: ") + hipGetErrorString(e));
     {
         std::vector<double> starts((size_t)kMaxRays * 3);
@@ -192,7 +199,13 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     int predict = 16, chunk = 64;
     std::vector<V3> sp(kMaxPix);
     std::vector<int> first(kMaxPix + 1);
+    // RT_SCREEN_PROFILE=1: host build / GPU round trip / resolve times and chunk counts on stderr.
+    const bool prof = getenv("RT_SCREEN_PROFILE") != nullptr;
+    using clk = std::chrono::steady_clock;
+    double t_build = 0, t_gpu = 0, t_res = 0;
+    long long n_chunks = 0, n_rays = 0;
     while (p < P) {
+        const auto c0 = clk::now();
         // Chunk: pixels p .. p+m-1, `predict` samples each.
         const int m = (int)std::min<long long>(std::min(chunk, kMaxRays / predict), P - p);
         V3 w = walk;
@@ -209,16 +222,15 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
             if ((int)(pix % W) == W - 1) w = (w - rightOffset) + up; // :1320-1321
         }
         first[m] = nr;
-        // One round trip: copy in, trace, copy out on one stream, one synchronisation.
-        e = hipMemcpyAsync(d_end.p, he, (size_t)nr * 3 * sizeof(double), hipMemcpyHostToDevice, st.s);
-        if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(e));
-        rc = rt_trace_rays_dev(ctx, static_cast<const double*>(d_start.p), static_cast<const double*>(d_end.p), nr,
-                               depth, static_cast<double*>(d_rgb.p), nullptr, st.s);
+        const auto c1 = clk::now();
+        // One round trip: the kernel reads the ends from and writes the colours to host memory.
+        rc = rt_trace_rays_dev(ctx, static_cast<const double*>(d_start.p), static_cast<const double*>(d_end), nr,
+                               depth, static_cast<double*>(d_rgb), nullptr, st.s);
         if (rc) return rc;
-        e = hipMemcpyAsync(h_rgb.p, d_rgb.p, (size_t)nr * 3 * sizeof(double), hipMemcpyDeviceToHost, st.s);
-        if (e == hipSuccess) e = hipStreamSynchronize(st.s);
+        e = hipStreamSynchronize(st.s);
         if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(e));
 
+        const auto c2 = clk::now();
         // Resolve in order with the reference's loop (:1294-1311).
         int q = 0;
         bool broke = false;
@@ -264,7 +276,18 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         p += q;
         jit.consume_until(S);
         chunk = broke ? std::max(16, chunk / 2) : std::min(kMaxPix, chunk * 2);
+        if (prof) {
+            const auto c3 = clk::now();
+            t_build += std::chrono::duration<double>(c1 - c0).count();
+            t_gpu += std::chrono::duration<double>(c2 - c1).count();
+            t_res += std::chrono::duration<double>(c3 - c2).count();
+            ++n_chunks;
+            n_rays += nr;
+        }
     }
+    if (prof)
+        fprintf(stderr, "rt_render_screen: %lld chunks, %lld rays traced; build %.1f ms, gpu %.1f ms, resolve %.1f ms\n",
+                n_chunks, n_rays, t_build * 1e3, t_gpu * 1e3, t_res * 1e3);
     if (rand_calls) *rand_calls = jit.consumed_calls;
     return RT_OK;
 }

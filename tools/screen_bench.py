@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Time the reference-faithful rayTraceScreen: rt_render_screen (GPU chunks) vs the serial C restatement
-(oracle/rt_oracle.c, one core — the frame is a serial chain).  usage: screen_bench.py [scene W H ...]"""
+(oracle/rt_oracle.c, one core — the frame is a serial chain).  RT_SCREEN_PROFILE=1 prints the phases.
+usage: screen_bench.py [scene W H ...]"""
 import ctypes
 import json
 import os
@@ -28,6 +29,10 @@ def main():
         rgb = np.zeros((H, W, 3), np.float64)
         ns = np.zeros((H, W), np.uint8)
         calls = ctypes.c_uint64()
+        # warm-up call (first launch of the trace kernel variant, host/device allocations), then timed
+        abi.check(abi.lib().rt_render_screen(tr._ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, 5, 0, 1,
+                                             rgb.ctypes.data, None, ns.ctypes.data, ctypes.byref(calls)),
+                  "rt_render_screen")
         t = time.perf_counter()
         abi.check(abi.lib().rt_render_screen(tr._ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, 5, 0, 1,
                                              rgb.ctypes.data, None, ns.ctypes.data, ctypes.byref(calls)),
