@@ -9,6 +9,8 @@
 #ifndef RT_DIAG_H
 #define RT_DIAG_H
 
+#include "rt_api.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -25,7 +27,6 @@ int rt_probe_math_dev(int op, const double* in, int n, double* out, void* stream
  * first render of a new (scene, camera, size, row plan, depth) times its 8-row tile rows and later
  * renders dispatch them longest first; mode 1 bottom-to-top.  Images are identical either way (every
  * tile is traced once, by the same code).  RT_EINVAL for another mode. */
-typedef struct rt_ctx rt_ctx;
 int rt_diag_tile_order(rt_ctx* ctx, int mode);
 
 #ifdef __cplusplus

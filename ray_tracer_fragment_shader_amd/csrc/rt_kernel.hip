@@ -40,6 +40,9 @@ using namespace rt;
 #ifndef RT_MINW
 #define RT_MINW 5
 #endif
+#ifndef RT_MINW_CULL
+#define RT_MINW_CULL RT_MINW                   // the culling variant (>= kConeMin spheres)
+#endif
 
 namespace {
 
@@ -709,7 +712,7 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
                 depth, grid, lds256, st, c->d_scene, P, o32, o8, rgb64f, raycount);
     else {
         // >= kConeMin spheres: the wave-culling variant (secondary and shadow rays, rt_device.hpp CULL).
-        auto launch = cull ? (mw5 ? launch_render_lds<0, RT_MINW, false, true, 64> : launch_render_lds<0, 1, false, true, 64>)
+        auto launch = cull ? (mw5 ? launch_render_lds<0, RT_MINW_CULL, false, true, 64> : launch_render_lds<0, 1, false, true, 64>)
                            : (mw5 ? launch_render_lds<0, RT_MINW, false, false, 64> : launch_render_lds<0, 1, false, false, 64>);
         e = launch(depth, grid, lds64, st, c->d_scene, P, o32, o8, rgb64f, raycount);
     }
