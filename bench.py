@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--scaling", default="weak", choices=["weak", "streams", "strong"])
     ap.add_argument("--band-height", type=int, default=0, help="0: auto (equal rows per rank)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--cpu-reps", type=int, default=3, help="minimum frames of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (wall seconds)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path on a one-GPU box (every rank on device 0, exchange staged "
                          "through host memory); the measured path is nccl (= RCCL)")
@@ -289,16 +290,18 @@ def main() -> int:
             from oracle import pyoracle as po
             nt = cpu_threads()
             sa = scene.to_abi()
-            best = float("inf")
-            for _ in range(args.cpu_reps):
-                t = time.perf_counter()
+            # bounded sample: whole frames, repeated until --cpu-seconds of wall time (at least --cpu-reps)
+            po.render(sa, cam, W, H, B, nthreads=nt)                 # warm (library load, page faults)
+            frames, t0c = 0, time.perf_counter()
+            while frames < args.cpu_reps or time.perf_counter() - t0c < args.cpu_seconds:
                 po.render(sa, cam, W, H, B, nthreads=nt)
-                best = min(best, time.perf_counter() - t)
+                frames += 1
+            spent = time.perf_counter() - t0c
             res["cpu_baseline"] = {
-                "value": round(rays_frame / best / 1e6, 3), "unit": "Mray/s", "cores": nt, "kind": "port",
-                "sample": f"full {cfg.name} frame ({W}x{H}, {rays_frame} rays) with oracle/rt_oracle.c "
-                          f"(bit-exact restatement, gcc -O2, OpenMP {nt} threads), best of {args.cpu_reps}; "
-                          f"{best * 1e3:.1f} ms/frame; host CPU: {cpu_model()}",
+                "value": round(rays_frame * frames / spent / 1e6, 3), "unit": "Mray/s", "cores": nt, "kind": "port",
+                "sample": f"{frames} full {cfg.name} frames ({W}x{H}, {rays_frame} rays each) back to back in "
+                          f"{spent:.1f} s with oracle/rt_oracle.c (bit-exact restatement, gcc -O2, OpenMP {nt} "
+                          f"threads); {spent / frames * 1e3:.1f} ms/frame; host CPU: {cpu_model()}",
             }
         print(json.dumps(res), flush=True)
     tr.close()
