@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -488,7 +489,7 @@ struct rt_ctx {
     uint32_t* d_row_cost = nullptr;
     int n_tile_rows = 0;                       // capacity of both (kOrderMax, allocated by rt_ctx_create)
     bool order_valid = false;
-    std::vector<unsigned char> order_key;
+    std::array<unsigned char, sizeof(rt_camera) + 6 * sizeof(int) + sizeof(rt_rows) + sizeof(uint64_t)> order_key{};
     int order_mode = 0;
     uint64_t scene_gen = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -662,7 +663,7 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     hipStream_t st0 = (hipStream_t)stream;
     if (c->order_mode == 0 && tiles_y <= c->n_tile_rows) {
         // Key of the frame's work: camera, size, outputs, row plan, depth and scene generation.
-        std::vector<unsigned char> key(sizeof(rt_camera) + 6 * sizeof(int) + sizeof(rt_rows) + sizeof(uint64_t), 0);
+        decltype(c->order_key) key{};                   // fixed size: no host allocation per render
         unsigned char* kp = key.data();
         memcpy(kp, cam, sizeof(rt_camera)); kp += sizeof(rt_camera);
         // which outputs are written changes the rows' relative cost (an RGB64F parity render writes
