@@ -41,6 +41,9 @@ using namespace rt;
 #ifndef RT_MINW
 #define RT_MINW 5
 #endif
+#ifndef RT_WG_FAST
+#define RT_WG_FAST 64                          // workgroup of the default render kernels: 64 (8 x 8) or 128 (16 x 8)
+#endif
 #ifndef RT_MINW_CULL
 #define RT_MINW_CULL RT_MINW                   // the culling variant (>= kConeMin spheres)
 #endif
@@ -656,7 +659,7 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     // waiting for three siblings).  The A/B variants that share a workgroup-wide LDS copy (scene in LDS,
     // staged row stores) keep 256 threads.
     const bool big = c->use_lds || c->wg_staging;
-    const int tw = big ? kTileW : 8;
+    const int tw = big ? kTileW : RT_WG_FAST / 8;
     const int tiles_x = (W + tw - 1) / tw;
     const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
     P.tile_rows_n = tiles_y;
@@ -713,9 +716,11 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
                 depth, grid, lds256, st, c->d_scene, P, o32, o8, rgb64f, raycount);
     else {
         // >= kConeMin spheres: the wave-culling variant (secondary and shadow rays, rt_device.hpp CULL).
-        auto launch = cull ? (mw5 ? launch_render_lds<0, RT_MINW_CULL, false, true, 64> : launch_render_lds<0, 1, false, true, 64>)
-                           : (mw5 ? launch_render_lds<0, RT_MINW, false, false, 64> : launch_render_lds<0, 1, false, false, 64>);
-        e = launch(depth, grid, lds64, st, c->d_scene, P, o32, o8, rgb64f, raycount);
+        auto launch = cull ? (mw5 ? launch_render_lds<0, RT_MINW_CULL, false, true, RT_WG_FAST>
+                                  : launch_render_lds<0, 1, false, true, RT_WG_FAST>)
+                           : (mw5 ? launch_render_lds<0, RT_MINW, false, false, RT_WG_FAST>
+                                  : launch_render_lds<0, 1, false, false, RT_WG_FAST>);
+        e = launch(depth, grid, slot_bytes(depth, false, RT_WG_FAST), st, c->d_scene, P, o32, o8, rgb64f, raycount);
     }
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_kernel launch: ") + hipGetErrorString(e));
     if (P.row_cost) {
