@@ -41,6 +41,9 @@ using namespace rt;
 #ifndef RT_MINW
 #define RT_MINW 5
 #endif
+#ifndef RT_NT_STORES
+#define RT_NT_STORES 0                         // 1: non-temporal RGBA32F/RGBA8 stores (A/B)
+#endif
 #ifndef RT_WG_FAST
 #define RT_WG_FAST 64                          // workgroup of the default render kernels: 64 (8 x 8) or 128 (16 x 8)
 #endif
@@ -193,10 +196,28 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
         // retires without waiting at a workgroup barrier for slower waves of the tile.
         if (valid) {
             const size_t k = (size_t)lr * P.width + i;
+#if RT_NT_STORES
+            if (out32) {
+                float* o = reinterpret_cast<float*>(out32 + k);
+                __builtin_nontemporal_store((float)col.x, o);
+                __builtin_nontemporal_store((float)col.y, o + 1);
+                __builtin_nontemporal_store((float)col.z, o + 2);
+                __builtin_nontemporal_store(1.0f, o + 3);
+            }
+#else
             if (out32) out32[k] = make_float4((float)col.x, (float)col.y, (float)col.z, 1.0f);
+#endif
             if (out64) { out64[3 * k] = col.x; out64[3 * k + 1] = col.y; out64[3 * k + 2] = col.z; }
             if (outrc) outrc[k] = seg | (sh << 16);
+#if RT_NT_STORES
+            if (out8) {
+                const uint32_t px = (uint32_t)to_u8(col.x) | ((uint32_t)to_u8(col.y) << 8) |
+                                    ((uint32_t)to_u8(col.z) << 16) | (255u << 24);
+                __builtin_nontemporal_store(px, reinterpret_cast<uint32_t*>(out8 + k));
+            }
+#else
             if (out8) out8[k] = make_uchar4(to_u8(col.x), to_u8(col.y), to_u8(col.z), 255);
+#endif
         }
         if (P.row_cost && tid == 0)
             atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
