@@ -133,7 +133,10 @@ def main() -> int:
     nl = plan.local[prank]                 # rows this rank renders per step (all its frames)
     fl = plan.frame_local[prank]           # ... per frame
     out32 = torch.empty((nl, W, 4), dtype=torch.float32, device=dev)
-    out8 = [torch.empty((nl, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
+    # RGBA8 slabs are double-buffered only where a step's exchange reads them while the next step renders
+    # (frame streams, strong gather); independent frames write one buffer.
+    out8 = [torch.empty((nl, W, 4), dtype=torch.uint8, device=dev) for _ in range(2 if banded else 1)]
+    out8 = out8 * (2 // len(out8))
     if streams:
         recv8 = [torch.empty((world, fl, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
         image8 = [torch.empty((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
