@@ -22,6 +22,11 @@
  *    asynchronous on the caller's stream and does not allocate, so it may be captured in a hipGraph.
  *    A context's renders must be stream-ordered (one stream at a time): a render may update the
  *    context's per-camera data (sphere data for a new eye, the tile-row dispatch order).
+ *  - hipGraph capture: a captured render is self-contained (it carries its own per-eye preparation and
+ *    uses the identity tile-row order), so renders of other views between replays do not disturb it.
+ *    rt_set_scene with a different scene invalidates captured graphs (the scene record may move).
+ *  - Multi-GPU: rt_group + rt_render_multi split a frame's rows over GPUs and gather
+ *    them to rank 0 over RCCL (one process driving several GPUs, or one process per GPU).
  */
 #ifndef RT_API_H
 #define RT_API_H
@@ -33,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 #define RT_OK            0
 #define RT_EINVAL       -1   /* bad argument (null pointer, size, unsupported material, ...) */
@@ -190,7 +195,11 @@ int rt_local_rows(int height, const rt_rows* rows, int* out);
 int rt_global_row(int height, const rt_rows* rows, int local_row, int* out);
 
 /* ---- device path ---------------------------------------------------------------------------- */
-/* Validate and upload the scene (scene + spheres + lights are copied; caller keeps ownership). */
+/* Validate and upload the scene (scene + spheres + lights are copied; caller keeps ownership).
+ * A scene identical to the uploaded one (same flattened record) is a no-op: no device work, the per-eye
+ * data and tile-row order are kept (rt_render calls this every frame).  A changed scene first waits for
+ * all work on the context's device (renders in flight on any stream read the old record), then uploads
+ * synchronously. */
 int rt_set_scene(rt_ctx* ctx, const rt_scene* scene);
 
 /* Render this rank's rows of a width x height frame with `depth` bounces (rayTraceRay's `depth`).
@@ -223,8 +232,11 @@ int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, i
                      int depth, int rand_kind, uint32_t seed, double* rgb64f, uint8_t* rgba8,
                      uint8_t* samples, uint64_t* rand_calls);
 
-/* Synchronous host-buffer convenience: uploads `scene`, renders, copies back, fills *stats
- * (ray counts + kernel time).  Any output pointer may be NULL. */
+/* Synchronous host-buffer convenience for draw() (MySdlApplication.cpp:1541-1563): uploads `scene` (a
+ * no-op when unchanged), renders into device buffers the context keeps between calls, copies back, fills
+ * *stats (ray counts summed on the device + kernel time).  Any output pointer may be NULL.  Tile-row order:
+ * the first render of a view uses the identity order, the second times its tile rows, later renders
+ * of the view dispatch the longest rows first (images are identical either way). */
 int rt_render(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, int width, int height,
               int depth, const rt_rows* rows, float* rgba32f, uint8_t* rgba8, double* rgb64f,
               rt_stats* stats);
@@ -242,6 +254,43 @@ int rt_trace_rays_dev(rt_ctx* ctx, const double* starts, const double* ends, int
  * elem_bytes in {1,2,4,8,16,24,32}: bytes per pixel. */
 int rt_unshuffle_dev(const void* gathered, void* image, int width, int height, int elem_bytes,
                      int band_height, int n_ranks, int slab_rows, void* stream);
+
+/* ---- multi-GPU: one frame's rows split over GPUs, gathered to rank 0 ---- */
+/* A group of ranks: rank r renders the round-robin row bands b = r (mod n_ranks) of every frame into its
+ * slab; rt_render_multi gathers the slabs to rank 0 (ncclSend / ncclRecv over xGMI) and puts the rows in
+ * image order there (rt_unshuffle_dev).  Slabs and rank 0's gather buffer are double-buffered and every rank
+ * renders and sends on the group's own streams, so frame f's gather overlaps frame f+1's render.
+ * Each rank renders its context's scene: call rt_set_scene on every context with the same scene. */
+#define RT_TRANSPORT_AUTO -1    /* RCCL when the contexts are on distinct devices, else COPY */
+#define RT_TRANSPORT_RCCL  0    /* RCCL send/recv (one communicator rank per context) */
+#define RT_TRANSPORT_COPY  1    /* hipMemcpyPeerAsync to rank 0 (contexts may share a device) */
+#define RT_OUT_RGBA32F 1
+#define RT_OUT_RGBA8   2
+#define RT_COMM_ID_BYTES 128
+typedef struct rt_group rt_group;
+/* Bands for n_ranks: band_height 0 = auto (largest height <= 16 that gives every rank the same rows, e.g.
+ * 15 for 1080 rows over 8 ranks; else 8).  *slab_rows_out (nullable) = the most rows any rank renders. */
+int rt_band_plan(int height, int n_ranks, int band_height, int* band_out, int* slab_rows_out);
+/* One process driving n GPUs: ctxs[q] is rank q (ctxs[0] receives the image); distinct contexts, each on
+ * its device (ncclCommInitAll over the contexts' devices for RT_TRANSPORT_RCCL). */
+int rt_group_create(rt_ctx* const* ctxs, int n, int transport, rt_group** out);
+/* One process per GPU (a torchrun-style launch): rank 0 makes the id, the launcher hands the same
+ * RT_COMM_ID_BYTES bytes to every rank, each rank passes its own context (ncclCommInitRank). */
+int rt_comm_unique_id(uint8_t* id);
+int rt_group_create_rank(rt_ctx* ctx, int n_ranks, int rank, const uint8_t* id, rt_group** out);
+int rt_group_destroy(rt_group* group);
+/* *n_ranks: ranks of the group; *n_local: ranks driven by this process; *first_rank: the first of them;
+ * *transport: RT_TRANSPORT_RCCL or RT_TRANSPORT_COPY.  Each pointer nullable. */
+int rt_group_info(const rt_group* group, int* n_ranks, int* n_local, int* first_rank, int* transport);
+/* One frame over the whole group.  Every rank calls it with the same camera, size, depth, band_height
+ * (0 = auto) and `outputs` (RT_OUT_RGBA32F | RT_OUT_RGBA8: what travels).  On rank 0, rgba32f / rgba8 are
+ * device images (width x height, j = 0 bottom) on rank 0's device for the requested outputs, assembled in
+ * order on `stream` (a hipStream_t of that device; NULL = default stream); other ranks' pointers are
+ * ignored.  Asynchronous: rank 0's image is complete when `stream` reaches this call's work. */
+int rt_render_multi(rt_group* group, const rt_camera* cam, int width, int height, int depth, int band_height,
+                    int outputs, float* rgba32f, uint8_t* rgba8, void* stream);
+/* Wait for the group's own render and gather streams (e.g. before timing on a rank > 0). */
+int rt_group_synchronize(rt_group* group);
 
 /* ---- output (host) -------------------------------------------------------------------------- */
 /* writePpmScreenshot format (Hw4/ppm.cpp:15-25): "P6 W H 255\n" then RGB rows top-down, from an

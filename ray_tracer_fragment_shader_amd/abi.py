@@ -26,6 +26,10 @@ RT_MAX_DEPTH = 7
 RT_RAND_GLIBC, RT_RAND_MSVC = 0, 1
 RT_MESH_TETRAHEDRON = 1
 RT_MESH_CUBE = 2
+ABI_VERSION = 4
+RT_TRANSPORT_AUTO, RT_TRANSPORT_RCCL, RT_TRANSPORT_COPY = -1, 0, 1
+RT_OUT_RGBA32F, RT_OUT_RGBA8 = 1, 2
+RT_COMM_ID_BYTES = 128
 
 D3 = c_double * 3
 
@@ -124,6 +128,15 @@ SIGNATURES = {
     "rt_write_ppm": (c_int, [c_char_p, _P(c_uint8), c_int, c_int, c_int]),
     "rt_render_screen": (c_int, [c_void_p, _P(rt_scene), _P(rt_camera), c_int, c_int, c_int, c_int, ctypes.c_uint32,
                                  c_void_p, c_void_p, c_void_p, _P(ctypes.c_uint64)]),
+    "rt_band_plan": (c_int, [c_int, c_int, c_int, _P(c_int), _P(c_int)]),
+    "rt_group_create": (c_int, [_P(c_void_p), c_int, c_int, _P(c_void_p)]),
+    "rt_comm_unique_id": (c_int, [c_void_p]),
+    "rt_group_create_rank": (c_int, [c_void_p, c_int, c_int, c_void_p, _P(c_void_p)]),
+    "rt_group_destroy": (c_int, [c_void_p]),
+    "rt_group_info": (c_int, [c_void_p, _P(c_int), _P(c_int), _P(c_int), _P(c_int)]),
+    "rt_render_multi": (c_int, [c_void_p, _P(rt_camera), c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                c_void_p]),
+    "rt_group_synchronize": (c_int, [c_void_p]),
     # include/rt_diag.h
     "rt_probe_math_dev": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "rt_diag_tile_order": (c_int, [c_void_p, c_int]),
@@ -147,7 +160,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.rt_abi_version() != 3:
+        if L.rt_abi_version() != ABI_VERSION:
             raise RuntimeError("librt_amd.so ABI version mismatch")
         _lib = L
     return _lib

@@ -13,6 +13,14 @@
 //   rt_render --config demo --faithful glibc|msvc [--seed S] --out demo_ref.ppm
 //                                                  rayTraceScreen exactly as the app runs it (jitter, up to
 //                                                  16 adaptive samples, colour carry-over): rt_render_screen
+//   rt_render --config c4 --gpus 8 [--band H] [--repeat K] --out c4.ppm
+//                                                  one frame's rows split over 8 GPUs (rt_group, RCCL gather to
+//                                                  GPU 0); with fewer GPUs than --gpus the
+//                                                  contexts share devices and the gather is a device copy
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -33,6 +41,9 @@ struct Options {
     double pitch = 0;
     int faithful = -1;                       // RT_RAND_GLIBC / RT_RAND_MSVC: rt_render_screen
     unsigned seed = 1;
+    int gpus = 0;                            // > 0: rt_group over this many ranks (rt_render_multi)
+    int band = 0;                            // band height (0: auto)
+    int repeat = 1;                          // frames rendered (the last one is written)
 };
 
 [[noreturn]] void die(const std::string& what, int code) {
@@ -89,6 +100,53 @@ Canonical canonical(const std::string& c) {
     std::exit(2);
 }
 
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "rt_render: %s failed: %s\n", what, hipGetErrorString(e));
+        std::exit(1);
+    }
+}
+
+// --gpus N: one context per rank on device q % (devices), one rt_group, rt_render_multi into an RGBA8 image
+// on rank 0's device (draw()'s frame, MySdlApplication.cpp:1541-1563, with its rows split over the GPUs).
+int render_multi(const Options& o, const rt_scene& scene, const rt_camera& cam, int W, int H, int depth) {
+    int ndev = 0;
+    check(rt_device_count(&ndev), "rt_device_count");
+    std::vector<rt_ctx*> ctxs(o.gpus, nullptr);
+    for (int q = 0; q < o.gpus; ++q) {
+        check(rt_ctx_create(q % ndev, &ctxs[q]), "rt_ctx_create");
+        check(rt_set_scene(ctxs[q], &scene), "rt_set_scene");
+    }
+    rt_group* g = nullptr;
+    check(rt_group_create(ctxs.data(), o.gpus, RT_TRANSPORT_AUTO, &g), "rt_group_create");
+    int transport = 0, band = 0, slab = 0;
+    check(rt_group_info(g, nullptr, nullptr, nullptr, &transport), "rt_group_info");
+    check(rt_band_plan(H, o.gpus, o.band, &band, &slab), "rt_band_plan");
+    hip_check(hipSetDevice(0), "hipSetDevice");
+    uint8_t* d8 = nullptr;
+    hip_check(hipMalloc(&d8, (size_t)W * H * 4), "hipMalloc");
+    hipStream_t st = nullptr;
+    hip_check(hipStreamCreate(&st), "hipStreamCreate");
+    check(rt_render_multi(g, &cam, W, H, depth, o.band, RT_OUT_RGBA8, nullptr, d8, st), "rt_render_multi");
+    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");                  // first frame (setup)
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < o.repeat; ++k)
+        check(rt_render_multi(g, &cam, W, H, depth, o.band, RT_OUT_RGBA8, nullptr, d8, st), "rt_render_multi");
+    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / o.repeat;
+    std::vector<uint8_t> rgba8((size_t)W * H * 4);
+    hip_check(hipMemcpy(rgba8.data(), d8, rgba8.size(), hipMemcpyDeviceToHost), "hipMemcpy");
+    check(rt_write_ppm(o.out.c_str(), rgba8.data(), W, H, 4), "rt_write_ppm");
+    std::printf("rt_render: %dx%d depth %d over %d ranks (%d device(s), band %d rows, %s gather to rank 0) -> %s | "
+                "%.3f ms per frame over %d frame(s)\n", W, H, depth, o.gpus, std::min(ndev, o.gpus), band,
+                transport == RT_TRANSPORT_RCCL ? "RCCL" : "device-copy", o.out.c_str(), ms, o.repeat);
+    rt_group_destroy(g);
+    (void)hipFree(d8);
+    (void)hipStreamDestroy(st);
+    for (auto* c : ctxs) rt_ctx_destroy(c);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -109,9 +167,12 @@ int main(int argc, char** argv) {
         else if (a == "--device") o.device = std::atoi(next().c_str());
         else if (a == "--faithful") o.faithful = next() == "msvc" ? RT_RAND_MSVC : RT_RAND_GLIBC;
         else if (a == "--seed") o.seed = (unsigned)std::strtoul(next().c_str(), nullptr, 10);
+        else if (a == "--gpus") o.gpus = std::atoi(next().c_str());
+        else if (a == "--band") o.band = std::atoi(next().c_str());
+        else if (a == "--repeat") o.repeat = std::max(1, std::atoi(next().c_str()));
         else { std::fprintf(stderr, "usage: rt_render [--config c1|c2|c3|c5|demo | --stdin] [--width W --height H "
                                     "--pitch P --depth B] [--device N] [--faithful glibc|msvc [--seed S]] "
-                                    "[--out file.ppm]\n"); return 2; }
+                                    "[--gpus N [--band H]] [--repeat K] [--out file.ppm]\n"); return 2; }
     }
 
     rt_scene scene;
@@ -212,8 +273,16 @@ int main(int argc, char** argv) {
         rt_ctx_destroy(ctx);
         return 0;
     }
+    if (o.gpus > 0) {
+        rt_ctx_destroy(ctx);
+        return render_multi(o, scene, cam, W, H, depth);
+    }
     rt_stats st;
-    check(rt_render(ctx, &scene, &cam, W, H, depth, nullptr, nullptr, rgba8.data(), nullptr, &st), "rt_render");
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < o.repeat; ++k)
+        check(rt_render(ctx, &scene, &cam, W, H, depth, nullptr, nullptr, rgba8.data(), nullptr, &st), "rt_render");
+    const double per_call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() /
+                               o.repeat;
     check(rt_write_ppm(o.out.c_str(), rgba8.data(), W, H, 4), "rt_write_ppm");
     const uint64_t rays = st.primary_rays + st.reflect_rays + st.shadow_rays;
     std::printf("rt_render: %dx%d depth %d -> %s | rays %llu (primary %llu, reflect %llu, shadow %llu) | kernel %.3f ms"
@@ -221,6 +290,7 @@ int main(int argc, char** argv) {
                 W, H, depth, o.out.c_str(), (unsigned long long)rays, (unsigned long long)st.primary_rays,
                 (unsigned long long)st.reflect_rays, (unsigned long long)st.shadow_rays, st.kernel_ms,
                 rays / (st.kernel_ms * 1e3));
+    if (o.repeat > 1) std::printf("rt_render: %d calls, %.3f ms per call (host to host)\n", o.repeat, per_call_ms);
     rt_ctx_destroy(ctx);
     return 0;
 }

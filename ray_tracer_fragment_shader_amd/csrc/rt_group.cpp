@@ -1,0 +1,419 @@
+// rt_group.cpp — multi-GPU frames: row bands rendered on every GPU of a group, gathered to rank 0 over
+// RCCL (xGMI) and put back in image order there (BASELINE.json configs c4).
+//
+// The reference renders one frame on one thread (rayTraceScreen, Hw4/MySdlApplication.cpp:1251-1324, called
+// by draw() at :1560); it has no distribution.  Pixels are independent (rayTraceRay :1184-1249 reads only the
+// scene), so a frame splits by rows: round-robin bands of `band_height` rows (contiguous stripes would be badly
+// imbalanced: sky rows are cheap, board rows are not), rank r rendering bands b = r (mod n) densely into its
+// slab (rt_rows).  The only data-path exchange is the gather of the slabs to rank 0:
+//
+//   render stream rs_r:  wait sent[r][b] -> rt_render_dev(rows of r) into slab[r][b] -> record rendered[r][b]
+//   comm stream   cs_r:  wait rendered[r][b] -> ncclSend(slab[r][b] -> rank 0)      -> record sent[r][b]
+//   root cs_0:           wait assembled[b]   -> ncclRecv(gathered[b] + q*slab <- q), q = 0..n-1 (q = 0: self)
+//                        -> record received[b]
+//   caller stream (root): wait received[b] -> rt_unshuffle_dev(gathered[b] -> image) -> record assembled[b]
+//
+// b = frame & 1: the slabs and the root's gather buffer are double-buffered, so frame f's gather overlaps
+// frame f+1's render.  Transports: RCCL (ncclCommInitAll for one process driving n GPUs, ncclCommInitRank
+// for one process per GPU) or COPY (hipMemcpyPeerAsync on the root's comm stream; used when contexts share
+// a device — RCCL refuses two ranks on one GPU — which is how the n-rank logic is exercised on one GPU).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "rt_internal.hpp"
+
+namespace {
+
+constexpr int kKinds = 2;                      // 0: RGBA32F (16 B/px), 1: RGBA8 (4 B/px)
+constexpr size_t kElem[kKinds] = {16, 4};
+
+struct Rank {
+    rt_ctx* ctx = nullptr;
+    int device = 0;
+    int rank = 0;
+    hipStream_t rs = nullptr, cs = nullptr;    // render / comm streams (on `device`)
+    hipEvent_t rendered[2] = {nullptr, nullptr};
+    hipEvent_t sent[2] = {nullptr, nullptr};   // on cs (RCCL) or on the root's comm stream (COPY)
+    bool sent_rec[2] = {false, false};
+    void* slab[2][kKinds] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    size_t slab_cap[2][kKinds] = {{0, 0}, {0, 0}};
+    ncclComm_t comm = nullptr;
+};
+
+}  // namespace
+
+struct rt_group {
+    int n_ranks = 0;                           // ranks of the whole group
+    int transport = RT_TRANSPORT_RCCL;
+    bool owns_root = false;                    // rank 0 is one of this process's ranks (ranks[0])
+    std::vector<Rank> ranks;                   // this process's ranks
+    // root only
+    void* gathered[2][kKinds] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    size_t gathered_cap[2][kKinds] = {{0, 0}, {0, 0}};
+    hipEvent_t received[2] = {nullptr, nullptr};
+    hipEvent_t assembled[2] = {nullptr, nullptr};
+    bool assembled_rec[2] = {false, false};
+    uint64_t frame = 0;
+    int last_band = 0, last_slab_rows = 0;
+};
+
+namespace {
+
+#define G_HIP(call)                                                                                   \
+    do {                                                                                              \
+        hipError_t e_ = (call);                                                                       \
+        if (e_ != hipSuccess) return rt_fail(RT_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define G_NCCL(call)                                                                                  \
+    do {                                                                                              \
+        ncclResult_t r_ = (call);                                                                     \
+        if (r_ != ncclSuccess) return rt_fail(RT_EHIP, std::string(#call) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+int grow(void** p, size_t* cap, size_t bytes) {
+    if (bytes <= *cap) return RT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, bytes) != hipSuccess) return rt_fail(RT_ENOMEM, "rt_render_multi: hipMalloc of a slab failed");
+    *cap = bytes;
+    return RT_OK;
+}
+
+int setup_rank(Rank* r, rt_ctx* ctx, int rank, hipEvent_t* sent_device_events) {
+    r->ctx = ctx;
+    r->rank = rank;
+    r->device = rt_ctx_device(ctx);
+    G_HIP(hipSetDevice(r->device));
+    G_HIP(hipStreamCreateWithFlags(&r->rs, hipStreamNonBlocking));
+    G_HIP(hipStreamCreateWithFlags(&r->cs, hipStreamNonBlocking));
+    for (int b = 0; b < 2; ++b) {
+        G_HIP(hipEventCreateWithFlags(&r->rendered[b], hipEventDisableTiming));
+        if (!sent_device_events) G_HIP(hipEventCreateWithFlags(&r->sent[b], hipEventDisableTiming));
+        else r->sent[b] = sent_device_events[b];
+    }
+    return RT_OK;
+}
+
+int setup_root_events(rt_group* g) {
+    G_HIP(hipSetDevice(g->ranks[0].device));
+    for (int b = 0; b < 2; ++b) {
+        G_HIP(hipEventCreateWithFlags(&g->received[b], hipEventDisableTiming));
+        G_HIP(hipEventCreateWithFlags(&g->assembled[b], hipEventDisableTiming));
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" int rt_band_plan(int height, int n_ranks, int band_height, int* band_out, int* slab_rows_out) {
+    if (height <= 0 || n_ranks <= 0 || band_height < 0 || !band_out)
+        return rt_fail(RT_EINVAL, "rt_band_plan: bad arguments");
+    int hb = band_height;
+    if (hb == 0) {
+        // Largest band height <= 16 giving every rank the same rows (e.g. 15 for 1080 rows over 8 ranks);
+        // 8 when no such height exists (ranks then differ by at most one band).
+        hb = 8;
+        for (int h = 16; h >= 1; --h)
+            if (height % (h * n_ranks) == 0) { hb = h; break; }
+    }
+    if (n_ranks == 1) hb = std::max(hb, 1);
+    int slab = 0;
+    for (int q = 0; q < n_ranks; ++q) {
+        rt_rows r = {hb, n_ranks, q, 1};
+        int nl = 0;
+        int rc = rt_local_rows(height, &r, &nl);
+        if (rc) return rc;
+        slab = std::max(slab, nl);
+    }
+    *band_out = hb;
+    if (slab_rows_out) *slab_rows_out = slab;
+    return RT_OK;
+}
+
+extern "C" int rt_comm_unique_id(uint8_t* id) {
+    if (!id) return rt_fail(RT_EINVAL, "rt_comm_unique_id: null id");
+    static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "RCCL unique id size");
+    ncclUniqueId u;
+    G_NCCL(ncclGetUniqueId(&u));
+    memcpy(id, &u, sizeof(u));
+    return RT_OK;
+}
+
+extern "C" int rt_group_destroy(rt_group* g) {
+    if (!g) return RT_OK;
+    for (auto& r : g->ranks) {
+        (void)hipSetDevice(r.device);
+        if (r.rs) (void)hipStreamSynchronize(r.rs);
+        if (r.cs) (void)hipStreamSynchronize(r.cs);
+    }
+    for (auto& r : g->ranks) {
+        (void)hipSetDevice(r.device);
+        if (r.comm) (void)ncclCommDestroy(r.comm);
+        for (int b = 0; b < 2; ++b) {
+            if (r.rendered[b]) (void)hipEventDestroy(r.rendered[b]);
+            if (r.sent[b] && g->transport == RT_TRANSPORT_RCCL) (void)hipEventDestroy(r.sent[b]);
+            for (int k = 0; k < kKinds; ++k)
+                if (r.slab[b][k]) (void)hipFree(r.slab[b][k]);
+        }
+        if (r.rs) (void)hipStreamDestroy(r.rs);
+        if (r.cs) (void)hipStreamDestroy(r.cs);
+    }
+    if (g->owns_root && !g->ranks.empty()) {
+        (void)hipSetDevice(g->ranks[0].device);
+        for (int b = 0; b < 2; ++b) {
+            if (g->received[b]) (void)hipEventDestroy(g->received[b]);
+            if (g->assembled[b]) (void)hipEventDestroy(g->assembled[b]);
+            for (int k = 0; k < kKinds; ++k)
+                if (g->gathered[b][k]) (void)hipFree(g->gathered[b][k]);
+        }
+        if (g->transport == RT_TRANSPORT_COPY)          // COPY: every rank's `sent` events live on the root
+            for (auto& r : g->ranks)
+                for (int b = 0; b < 2; ++b)
+                    if (r.sent[b]) (void)hipEventDestroy(r.sent[b]);
+    }
+    delete g;
+    return RT_OK;
+}
+
+extern "C" int rt_group_create(rt_ctx* const* ctxs, int n, int transport, rt_group** out) {
+    if (!out) return rt_fail(RT_EINVAL, "rt_group_create: null out");
+    *out = nullptr;
+    if (!ctxs || n <= 0) return rt_fail(RT_EINVAL, "rt_group_create: need at least one context");
+    if (transport != RT_TRANSPORT_AUTO && transport != RT_TRANSPORT_RCCL && transport != RT_TRANSPORT_COPY)
+        return rt_fail(RT_EINVAL, "rt_group_create: unknown transport");
+    std::vector<int> devs(n);
+    for (int q = 0; q < n; ++q) {
+        if (!ctxs[q]) return rt_fail(RT_EINVAL, "rt_group_create: null context");
+        for (int p = 0; p < q; ++p)
+            if (ctxs[p] == ctxs[q]) return rt_fail(RT_EINVAL, "rt_group_create: a context appears twice");
+        devs[q] = rt_ctx_device(ctxs[q]);
+    }
+    std::vector<int> sorted = devs;
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    if (transport == RT_TRANSPORT_AUTO) transport = distinct ? RT_TRANSPORT_RCCL : RT_TRANSPORT_COPY;
+    if (transport == RT_TRANSPORT_RCCL && !distinct)
+        return rt_fail(RT_EINVAL, "rt_group_create: RCCL needs one context per device (use RT_TRANSPORT_COPY)");
+    rt_group* g = new rt_group();
+    g->n_ranks = n;
+    g->transport = transport;
+    g->owns_root = true;
+    g->ranks.resize(n);
+    int rc = RT_OK;
+    // COPY: the root's comm stream records every rank's `sent` events, so they live on the root device.
+    std::vector<hipEvent_t> root_sent(2 * n, nullptr);
+    if (transport == RT_TRANSPORT_COPY) {
+        if (hipSetDevice(devs[0]) != hipSuccess) { delete g; return rt_fail(RT_EHIP, "rt_group_create: hipSetDevice"); }
+        for (int q = 0; q < n; ++q)
+            for (int b = 0; b < 2; ++b) {
+                if (hipEventCreateWithFlags(&root_sent[2 * q + b], hipEventDisableTiming) != hipSuccess)
+                    rc = rt_fail(RT_EHIP, "rt_group_create: hipEventCreate failed");
+                g->ranks[q].sent[b] = root_sent[2 * q + b];    // owned by the group from here on
+            }
+    }
+    for (int q = 0; q < n && rc == RT_OK; ++q)
+        rc = setup_rank(&g->ranks[q], ctxs[q], q, transport == RT_TRANSPORT_COPY ? &root_sent[2 * q] : nullptr);
+    if (rc == RT_OK) rc = setup_root_events(g);
+    if (rc == RT_OK && transport == RT_TRANSPORT_RCCL) {
+        std::vector<ncclComm_t> comms(n);
+        ncclResult_t r = ncclCommInitAll(comms.data(), n, devs.data());
+        if (r != ncclSuccess) rc = rt_fail(RT_EHIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+        else
+            for (int q = 0; q < n; ++q) g->ranks[q].comm = comms[q];
+    }
+    if (rc != RT_OK) {
+        rt_group_destroy(g);
+        return rc;
+    }
+    *out = g;
+    return RT_OK;
+}
+
+extern "C" int rt_group_create_rank(rt_ctx* ctx, int n_ranks, int rank, const uint8_t* id, rt_group** out) {
+    if (!out) return rt_fail(RT_EINVAL, "rt_group_create_rank: null out");
+    *out = nullptr;
+    if (!ctx || !id || n_ranks <= 0 || rank < 0 || rank >= n_ranks)
+        return rt_fail(RT_EINVAL, "rt_group_create_rank: bad arguments");
+    rt_group* g = new rt_group();
+    g->n_ranks = n_ranks;
+    g->transport = RT_TRANSPORT_RCCL;
+    g->owns_root = rank == 0;
+    g->ranks.resize(1);
+    int rc = setup_rank(&g->ranks[0], ctx, rank, nullptr);
+    if (rc == RT_OK && g->owns_root) rc = setup_root_events(g);
+    if (rc == RT_OK) {
+        ncclUniqueId u;
+        memcpy(&u, id, sizeof(u));
+        (void)hipSetDevice(g->ranks[0].device);
+        ncclResult_t r = ncclCommInitRank(&g->ranks[0].comm, n_ranks, u, rank);
+        if (r != ncclSuccess) rc = rt_fail(RT_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    if (rc != RT_OK) {
+        rt_group_destroy(g);
+        return rc;
+    }
+    *out = g;
+    return RT_OK;
+}
+
+extern "C" int rt_group_info(const rt_group* g, int* n_ranks, int* n_local, int* first_rank, int* transport) {
+    if (!g) return rt_fail(RT_EINVAL, "rt_group_info: null group");
+    if (n_ranks) *n_ranks = g->n_ranks;
+    if (n_local) *n_local = (int)g->ranks.size();
+    if (first_rank) *first_rank = g->ranks.empty() ? 0 : g->ranks[0].rank;
+    if (transport) *transport = g->transport;
+    return RT_OK;
+}
+
+extern "C" int rt_group_synchronize(rt_group* g) {
+    if (!g) return rt_fail(RT_EINVAL, "rt_group_synchronize: null group");
+    for (auto& r : g->ranks) {
+        G_HIP(hipSetDevice(r.device));
+        G_HIP(hipStreamSynchronize(r.rs));
+        G_HIP(hipStreamSynchronize(r.cs));
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, int depth, int band_height,
+                               int outputs, float* rgba32f, uint8_t* rgba8, void* stream) {
+    if (!g) return rt_fail(RT_EINVAL, "rt_render_multi: null group");
+    if (!cam) return rt_fail(RT_EINVAL, "rt_render_multi: null camera");
+    if (W <= 0 || H <= 0) return rt_fail(RT_EINVAL, "rt_render_multi: bad image size");
+    if (outputs <= 0 || (outputs & ~(RT_OUT_RGBA32F | RT_OUT_RGBA8)))
+        return rt_fail(RT_EINVAL, "rt_render_multi: outputs must be a non-empty set of RT_OUT_RGBA32F | RT_OUT_RGBA8");
+    // Every rank passes the same `outputs` (it decides what travels); only rank 0's image pointers are used.
+    const bool kind_on[kKinds] = {(outputs & RT_OUT_RGBA32F) != 0, (outputs & RT_OUT_RGBA8) != 0};
+    void* outs[kKinds] = {rgba32f, rgba8};
+    if (g->owns_root && ((kind_on[0] && !rgba32f) || (kind_on[1] && !rgba8)))
+        return rt_fail(RT_EINVAL, "rt_render_multi: rank 0 needs a device image for every requested output");
+    int hb = 0, slab_rows = 0;
+    int rc = rt_band_plan(H, g->n_ranks, band_height, &hb, &slab_rows);
+    if (rc) return rc;
+    const int b = (int)(g->frame & 1);
+    const hipStream_t st = (hipStream_t)stream;
+
+    // ---- buffers (grow-only; a size change waits for the frames still using them) -----------------------
+    const bool regrow = hb != g->last_band || slab_rows != g->last_slab_rows;
+    if (regrow && g->frame > 0) {
+        rc = rt_group_synchronize(g);
+        if (rc) return rc;
+        if (g->owns_root) {
+            G_HIP(hipSetDevice(g->ranks[0].device));
+            G_HIP(hipStreamSynchronize(st));
+        }
+    }
+    g->last_band = hb;
+    g->last_slab_rows = slab_rows;
+    for (auto& r : g->ranks) {
+        G_HIP(hipSetDevice(r.device));
+        for (int k = 0; k < kKinds; ++k)
+            if (kind_on[k] && (rc = grow(&r.slab[b][k], &r.slab_cap[b][k], (size_t)slab_rows * W * kElem[k])))
+                return rc;
+    }
+    if (g->owns_root) {
+        G_HIP(hipSetDevice(g->ranks[0].device));
+        for (int k = 0; k < kKinds; ++k)
+            if (kind_on[k] && (rc = grow(&g->gathered[b][k], &g->gathered_cap[b][k],
+                                         (size_t)g->n_ranks * slab_rows * W * kElem[k])))
+                return rc;
+    }
+
+    // ---- render: every local rank's bands into slab[b] ------------------------------------------------------
+    for (auto& r : g->ranks) {
+        G_HIP(hipSetDevice(r.device));
+        if (r.sent_rec[b]) G_HIP(hipStreamWaitEvent(r.rs, r.sent[b], 0));     // slab[b] has left (frame - 2)
+        rt_rows rows = {hb, g->n_ranks, r.rank, 1};
+        rc = rt_render_dev(r.ctx, cam, W, H, depth, &rows, (float*)r.slab[b][0], (uint8_t*)r.slab[b][1], nullptr,
+                           nullptr, r.rs);
+        if (rc) return rc;
+        G_HIP(hipSetDevice(r.device));
+        G_HIP(hipEventRecord(r.rendered[b], r.rs));
+    }
+
+    // ---- gather to rank 0 ------------------------------------------------------------------------------------
+    auto rows_of = [&](int q) {
+        rt_rows rr = {hb, g->n_ranks, q, 1};
+        int nl = 0;
+        rt_local_rows(H, &rr, &nl);
+        return nl;
+    };
+    if (g->owns_root) {
+        Rank& root = g->ranks[0];
+        G_HIP(hipSetDevice(root.device));
+        if (g->assembled_rec[b]) G_HIP(hipStreamWaitEvent(root.cs, g->assembled[b], 0));   // gathered[b] is free
+    }
+    if (g->transport == RT_TRANSPORT_RCCL) {
+        for (auto& r : g->ranks) {
+            G_HIP(hipSetDevice(r.device));
+            G_HIP(hipStreamWaitEvent(r.cs, r.rendered[b], 0));
+        }
+        G_NCCL(ncclGroupStart());
+        for (auto& r : g->ranks) {
+            for (int k = 0; k < kKinds; ++k) {
+                if (!kind_on[k]) continue;
+                const size_t bytes = (size_t)rows_of(r.rank) * W * kElem[k];
+                ncclResult_t e = ncclSend(r.slab[b][k], bytes, ncclUint8, 0, r.comm, r.cs);
+                if (e != ncclSuccess) {
+                    (void)ncclGroupEnd();
+                    return rt_fail(RT_EHIP, std::string("ncclSend: ") + ncclGetErrorString(e));
+                }
+                if (r.rank != 0) continue;
+                for (int q = 0; q < g->n_ranks; ++q) {
+                    char* dst = (char*)g->gathered[b][k] + (size_t)q * slab_rows * W * kElem[k];
+                    e = ncclRecv(dst, (size_t)rows_of(q) * W * kElem[k], ncclUint8, q, r.comm, r.cs);
+                    if (e != ncclSuccess) {
+                        (void)ncclGroupEnd();
+                        return rt_fail(RT_EHIP, std::string("ncclRecv: ") + ncclGetErrorString(e));
+                    }
+                }
+            }
+        }
+        G_NCCL(ncclGroupEnd());
+        for (auto& r : g->ranks) {
+            G_HIP(hipSetDevice(r.device));
+            G_HIP(hipEventRecord(r.sent[b], r.cs));
+            r.sent_rec[b] = true;
+        }
+    } else {
+        Rank& root = g->ranks[0];
+        G_HIP(hipSetDevice(root.device));
+        for (auto& r : g->ranks) {
+            G_HIP(hipStreamWaitEvent(root.cs, r.rendered[b], 0));
+            for (int k = 0; k < kKinds; ++k) {
+                if (!kind_on[k]) continue;
+                char* dst = (char*)g->gathered[b][k] + (size_t)r.rank * slab_rows * W * kElem[k];
+                G_HIP(hipMemcpyPeerAsync(dst, root.device, r.slab[b][k], r.device,
+                                         (size_t)rows_of(r.rank) * W * kElem[k], root.cs));
+            }
+            G_HIP(hipEventRecord(r.sent[b], root.cs));
+            r.sent_rec[b] = true;
+        }
+    }
+
+    // ---- assemble on rank 0, ordered on the caller's stream --------------------------------------------------
+    if (g->owns_root) {
+        Rank& root = g->ranks[0];
+        G_HIP(hipSetDevice(root.device));
+        G_HIP(hipEventRecord(g->received[b], root.cs));
+        G_HIP(hipStreamWaitEvent(st, g->received[b], 0));
+        for (int k = 0; k < kKinds; ++k) {
+            if (!kind_on[k]) continue;
+            rc = rt_unshuffle_dev(g->gathered[b][k], outs[k], W, H, (int)kElem[k], hb, g->n_ranks, slab_rows, st);
+            if (rc) return rc;
+        }
+        G_HIP(hipEventRecord(g->assembled[b], st));
+        g->assembled_rec[b] = true;
+    }
+    ++g->frame;
+    return RT_OK;
+}

@@ -16,3 +16,6 @@ int rt_build_dev_scene(const rt_scene* scene, std::vector<unsigned char>* blob);
 // rayTraceScreen basis (MySdlApplication.cpp:1270-1277): right = normalize(LD x up),
 // up' = normalize(right x LD), LD = look_at - eye.
 void rt_camera_basis(const rt_camera* cam, double right[3], double upp[3]);
+
+// Device ordinal of a context (rt_group.cpp).
+int rt_ctx_device(const rt_ctx* ctx);

@@ -161,7 +161,7 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
     const int tx = blockIdx.x;                      // 2-D grid: tiles_x x tiles_y
     const int gy = (int)(blockIdx.z * kGridY + blockIdx.y);    // tile rows beyond kGridY go to grid.z
     const int ty = P.tile_rows ? P.tile_rows[gy] : gy;
-    if (ty >= P.tile_rows_n) return;                            // padding of the last grid.z slice
+    if ((unsigned)ty >= (unsigned)P.tile_rows_n) return;        // padding of the last grid.z slice
     const int i = tx * TW + cx;
     const int lr = ty * kTileH + cy;
     const bool valid = i < P.width && lr < P.local_rows;
@@ -421,6 +421,26 @@ __global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* 
     for (int w = threadIdx.x; w < row_words; w += kThreads) d[w] = s[w];
 }
 
+// rt_render's ray statistics: sums of the per-pixel counters (primary+reflect segments, shadow rays) into
+// sums[0], sums[1] (zeroed by the caller), so only 16 bytes cross PCIe instead of 4 bytes per pixel.
+__global__ __launch_bounds__(kThreads) void rt_raysum_kernel(const uint32_t* __restrict__ rc, size_t n,
+                                                             unsigned long long* __restrict__ sums) {
+    unsigned long long seg = 0, sh = 0;
+    for (size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x; k < n; k += (size_t)gridDim.x * kThreads) {
+        const uint32_t v = rc[k];
+        seg += v & 0xffffu;
+        sh += v >> 16;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        seg += __shfl_down(seg, o);
+        sh += __shfl_down(sh, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(sums, seg);
+        atomicAdd(sums + 1, sh);
+    }
+}
+
 // Diagnostics (include/rt_diag.h): the exact-arithmetic fast paths of rt_device.hpp beside the compiler's
 // IEEE sequences, on caller-supplied operands.  op 0: per vector v (3 doubles) -> 9 doubles
 // [divs(v, len(v)), len(v), unit(v), |v| from unit(), len_fast(v)]; op 1: per pair (a, b) -> 2 doubles
@@ -501,22 +521,33 @@ struct rt_ctx {
     bool scene_set = false;
     bool transparent = false;                  // some material is transparent: TRANSP kernel variants
     bool eye_valid = false;                    // the device *Prim arrays hold data for `eye`
+    bool ever_captured = false;                // a render was captured into a hipGraph: replays may rewrite
+                                               // the per-eye data, so every later render re-prepares it
     double eye[3] = {0, 0, 0};
+    std::vector<unsigned char> blob;           // host image of d_scene (rt_set_scene skips an unchanged scene)
     int min_waves = 5;                         // __launch_bounds__(256, 5) for depth <= 3 (measured faster
                                                // despite small spills: tools/ab.py); RT_MIN_WAVES=0 disables
     int use_lds = 0;                           // RT_SCENE_IN_LDS=1: header + exact records in LDS (A/B: tools/ab.py)
     int wg_staging = 0;                        // RT_WG_STAGING=1: LDS-staged 32-pixel row stores (A/B)
     // Adaptive tile-row order (rt_order_kernel): the first render of a new (scene, camera, size, rows,
-    // depth) is a calibration render that also times its tile rows; later renders dispatch the rows by
-    // decreasing time.  order_mode (rt_diag_tile_order): 0 adaptive, 1 bottom-to-top.
+    // depth, outputs) view uses the identity order; the second render of the same view is a calibration
+    // render that also times its tile rows; later renders dispatch the rows by decreasing time (a camera
+    // that moves every frame never pays for a calibration).  order_mode (rt_diag_tile_order): 0 adaptive,
+    // 1 bottom-to-top.
     int32_t* d_tile_rows = nullptr;
     uint32_t* d_row_cost = nullptr;
     int n_tile_rows = 0;                       // capacity of both (kOrderMax, allocated by rt_ctx_create)
-    bool order_valid = false;
-    std::array<unsigned char, sizeof(rt_camera) + 6 * sizeof(int) + sizeof(rt_rows) + sizeof(uint64_t)> order_key{};
+    using ViewKey = std::array<unsigned char, sizeof(rt_camera) + 6 * sizeof(int) + sizeof(rt_rows) + sizeof(uint64_t)>;
+    bool order_valid = false;                  // d_tile_rows holds the order of view `order_key`
+    ViewKey order_key{};
+    bool seen_valid = false;                   // `seen_key`: the last view rendered once in identity order
+    ViewKey seen_key{};
     int order_mode = 0;
     uint64_t scene_gen = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // rt_render's device buffers (grow-only, reused across calls): rgba32f, rgba8, rgb64f, raycount, sums
+    void* d_out[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t out_cap[5] = {0, 0, 0, 0, 0};
 };
 
 #define RT_HIP(call)                                                                                  \
@@ -563,6 +594,10 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
         return rt_fail(RT_ENOMEM, "rt_ctx_create: hipMalloc of the tile-row order failed");
     }
     c->n_tile_rows = kOrderMax;
+    if (hipMemset(c->d_tile_rows, 0, sizeof(int32_t) * kOrderMax) != hipSuccess) {
+        rt_ctx_destroy(c);
+        return rt_fail(RT_EHIP, "rt_ctx_create: hipMemset of the tile-row order failed");
+    }
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         delete c;
         return rt_fail(RT_EHIP, "rt_ctx_create: hipEventCreate failed");
@@ -570,6 +605,8 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     *out = c;
     return RT_OK;
 }
+
+int rt_ctx_device(const rt_ctx* c) { return c ? c->device : -1; }
 
 extern "C" int rt_ctx_destroy(rt_ctx* c) {
     if (!c) return RT_OK;
@@ -579,6 +616,8 @@ extern "C" int rt_ctx_destroy(rt_ctx* c) {
     if (c->d_row_cost) (void)hipFree(c->d_row_cost);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (void* p : c->d_out)
+        if (p) (void)hipFree(p);
     delete c;
     return RT_OK;
 }
@@ -588,7 +627,13 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     std::vector<unsigned char> blob;
     int rc = rt_build_dev_scene(scene, &blob);
     if (rc) return rc;
+    // An unchanged scene (same flattened record, byte for byte) keeps the device copy, the per-eye data
+    // and the tile-row order: rt_render calls this every frame.
+    if (c->scene_set && blob == c->blob) return RT_OK;
     RT_HIP(hipSetDevice(c->device));
+    // Renders still in flight on any stream of this device read d_scene: wait for them before it changes.
+    RT_HIP(hipDeviceSynchronize());
+    c->scene_set = false;
     if (blob.size() > c->scene_cap) {
         if (c->d_scene) RT_HIP(hipFree(c->d_scene));
         c->d_scene = nullptr;
@@ -610,6 +655,7 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     c->transparent = h->transparent != 0 || h->n_meshes > 0;   // FULL kernel variants
     c->eye_valid = false;
     c->scene_set = true;
+    c->blob.swap(blob);
     ++c->scene_gen;
     return RT_OK;
 }
@@ -684,11 +730,18 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     const int tiles_x = (W + tw - 1) / tw;
     const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
     P.tile_rows_n = tiles_y;
-    hipStream_t st0 = (hipStream_t)stream;
-    if (c->order_mode == 0 && tiles_y <= c->n_tile_rows) {
+    hipStream_t st = (hipStream_t)stream;
+    // A render captured into a hipGraph must be self-contained: it always prepares its eye's data and uses
+    // the identity tile-row order (the context's order buffer belongs to whatever view it last calibrated).
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    RT_HIP(hipStreamIsCapturing(st, &cap));
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    if (capturing) c->ever_captured = true;
+    bool calibrate = false;
+    rt_ctx::ViewKey key{};
+    if (!capturing && c->order_mode == 0 && tiles_y <= c->n_tile_rows) {
         // Key of the frame's work: camera, size, outputs, row plan, depth and scene generation.
-        decltype(c->order_key) key{};                   // fixed size: no host allocation per render
-        unsigned char* kp = key.data();
+        unsigned char* kp = key.data();                 // fixed size: no host allocation per render
         memcpy(kp, cam, sizeof(rt_camera)); kp += sizeof(rt_camera);
         // which outputs are written changes the rows' relative cost (an RGB64F parity render writes
         // 24 B per pixel): each output set gets its own calibration
@@ -700,27 +753,29 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
         memcpy(kp, &c->scene_gen, sizeof(uint64_t));
         if (c->order_valid && key == c->order_key) {
             P.tile_rows = c->d_tile_rows;
-        } else {
-            RT_HIP(hipMemsetAsync(c->d_row_cost, 0, sizeof(uint32_t) * tiles_y, st0));
+        } else if (c->seen_valid && key == c->seen_key) {
+            RT_HIP(hipMemsetAsync(c->d_row_cost, 0, sizeof(uint32_t) * tiles_y, st));
             P.row_cost = c->d_row_cost;                 // calibration render (identity order)
-            c->order_key = key;
-            c->order_valid = true;
+            calibrate = true;
+            c->order_valid = false;                     // rt_order_kernel rewrites d_tile_rows below
+        } else {
+            c->seen_key = key;                          // first render of this view: identity order
+            c->seen_valid = true;
         }
     }
     dim3 grid((unsigned)tiles_x, (unsigned)std::min(tiles_y, kGridY), (unsigned)((tiles_y + kGridY - 1) / kGridY));
     const size_t lds64 = slot_bytes(depth, c->transparent, 64);
     const size_t lds256 = (c->wg_staging ? 4096 + 6144 + 1024 + 1024 : 0) + slot_bytes(depth, c->transparent);
-    hipStream_t st = (hipStream_t)stream;
     hipError_t e;
-    // Primary-ray sphere data for this eye (stream-ordered; only when the eye changes).
-    if (!c->eye_valid || memcmp(c->eye, cam->eye, sizeof(c->eye)) != 0) {
-        {
-            dim3 pg((unsigned)((std::max(c->n_padded, 1) + kThreads - 1) / kThreads));
-            hipLaunchKernelGGL(rt_prepare_kernel, pg, dim3(kThreads), 0, st, c->d_scene, cam->eye[0], cam->eye[1],
-                               cam->eye[2]);
-            e = hipGetLastError();
-            if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_prepare_kernel: ") + hipGetErrorString(e));
-        }
+    // Primary-ray sphere data for this eye (stream-ordered; only when the eye changes, or always once graphs
+    // that carry their own prepare launch exist).
+    if (capturing || c->ever_captured || !c->eye_valid || memcmp(c->eye, cam->eye, sizeof(c->eye)) != 0) {
+        c->eye_valid = false;
+        dim3 pg((unsigned)((std::max(c->n_padded, 1) + kThreads - 1) / kThreads));
+        hipLaunchKernelGGL(rt_prepare_kernel, pg, dim3(kThreads), 0, st, c->d_scene, cam->eye[0], cam->eye[1],
+                           cam->eye[2]);
+        e = hipGetLastError();
+        if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_prepare_kernel: ") + hipGetErrorString(e));
         memcpy(c->eye, cam->eye, sizeof(c->eye));
         c->eye_valid = true;
     }
@@ -744,61 +799,74 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
         e = launch(depth, grid, slot_bytes(depth, false, RT_WG_FAST), st, c->d_scene, P, o32, o8, rgb64f, raycount);
     }
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_kernel launch: ") + hipGetErrorString(e));
-    if (P.row_cost) {
+    if (calibrate) {
         hipLaunchKernelGGL(rt_order_kernel, dim3(1), dim3(1024), 0, st, c->d_row_cost, tiles_y, c->d_tile_rows);
         e = hipGetLastError();
         if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_order_kernel: ") + hipGetErrorString(e));
+        c->order_key = key;                             // only once the order kernel is queued
+        c->order_valid = true;
     }
+    return RT_OK;
+}
+
+// Grow-only device buffer k of the context (rt_render's outputs).
+static int ctx_buffer(rt_ctx* c, int k, size_t bytes, void** out) {
+    if (bytes > c->out_cap[k]) {
+        if (c->d_out[k]) (void)hipFree(c->d_out[k]);
+        c->d_out[k] = nullptr;
+        c->out_cap[k] = 0;
+        if (hipMalloc(&c->d_out[k], bytes) != hipSuccess)
+            return rt_fail(RT_ENOMEM, "rt_render: hipMalloc of output buffers failed");
+        c->out_cap[k] = bytes;
+    }
+    *out = c->d_out[k];
     return RT_OK;
 }
 
 extern "C" int rt_render(rt_ctx* c, const rt_scene* scene, const rt_camera* cam, int W, int H, int depth,
                          const rt_rows* rows, float* rgba32f, uint8_t* rgba8, double* rgb64f, rt_stats* stats) {
     if (!c) return rt_fail(RT_EINVAL, "rt_render: null context");
-    int rc = rt_set_scene(c, scene);
+    int rc = rt_set_scene(c, scene);                    // no device work when the scene is unchanged
     if (rc) return rc;
     RenderParams P;
     rc = render_params(c, cam, W, H, depth, rows, &P);
     if (rc) return rc;
+    RT_HIP(hipSetDevice(c->device));
     const size_t npx = (size_t)P.local_rows * W;
-    float* d32 = nullptr;
-    uint8_t* d8 = nullptr;
-    double* d64 = nullptr;
-    uint32_t* drc = nullptr;
-    auto cleanup = [&]() {
-        if (d32) (void)hipFree(d32);
-        if (d8) (void)hipFree(d8);
-        if (d64) (void)hipFree(d64);
-        if (drc) (void)hipFree(drc);
-    };
-    if ((rgba32f && hipMalloc(&d32, npx * 16) != hipSuccess) || (rgba8 && hipMalloc(&d8, npx * 4) != hipSuccess) ||
-        (rgb64f && hipMalloc(&d64, npx * 24) != hipSuccess) || (stats && hipMalloc(&drc, npx * 4) != hipSuccess)) {
-        cleanup();
-        return rt_fail(RT_ENOMEM, "rt_render: hipMalloc of output buffers failed");
-    }
+    void* d[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    const size_t bytes[5] = {npx * 16, npx * 4, npx * 24, npx * 4, 2 * sizeof(unsigned long long)};
+    const bool want[5] = {rgba32f != nullptr, rgba8 != nullptr, rgb64f != nullptr, stats != nullptr, stats != nullptr};
+    for (int k = 0; k < 5; ++k)
+        if (want[k] && npx > 0 && (rc = ctx_buffer(c, k, bytes[k], &d[k])) != RT_OK) return rc;
     hipError_t e = hipEventRecord(c->ev0, nullptr);
     if (e == hipSuccess) {
-        rc = rt_render_dev(c, cam, W, H, depth, rows, d32, d8, d64, drc, nullptr);
-        if (rc) { cleanup(); return rc; }
+        rc = rt_render_dev(c, cam, W, H, depth, rows, (float*)d[0], (uint8_t*)d[1], (double*)d[2], (uint32_t*)d[3],
+                           nullptr);
+        if (rc) return rc;
         e = hipEventRecord(c->ev1, nullptr);
     }
+    if (e == hipSuccess && stats && npx > 0) {
+        e = hipMemsetAsync(d[4], 0, bytes[4], nullptr);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(rt_raysum_kernel, dim3((unsigned)std::min<size_t>((npx + kThreads - 1) / kThreads, 1024)),
+                               dim3(kThreads), 0, nullptr, (const uint32_t*)d[3], npx, (unsigned long long*)d[4]);
+            e = hipGetLastError();
+        }
+    }
+    if (e == hipSuccess && rgba32f && npx) e = hipMemcpy(rgba32f, d[0], bytes[0], hipMemcpyDeviceToHost);
+    if (e == hipSuccess && rgba8 && npx) e = hipMemcpy(rgba8, d[1], bytes[1], hipMemcpyDeviceToHost);
+    if (e == hipSuccess && rgb64f && npx) e = hipMemcpy(rgb64f, d[2], bytes[2], hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e == hipSuccess && rgba32f) e = hipMemcpy(rgba32f, d32, npx * 16, hipMemcpyDeviceToHost);
-    if (e == hipSuccess && rgba8) e = hipMemcpy(rgba8, d8, npx * 4, hipMemcpyDeviceToHost);
-    if (e == hipSuccess && rgb64f) e = hipMemcpy(rgb64f, d64, npx * 24, hipMemcpyDeviceToHost);
     if (e == hipSuccess && stats) {
-        std::vector<uint32_t> h(npx);
-        e = hipMemcpy(h.data(), drc, npx * 4, hipMemcpyDeviceToHost);
-        uint64_t seg = 0, sh = 0;
-        for (uint32_t v : h) { seg += v & 0xffffu; sh += v >> 16; }
+        unsigned long long sums[2] = {0, 0};
+        if (npx) e = hipMemcpy(sums, d[4], sizeof(sums), hipMemcpyDeviceToHost);
         stats->primary_rays = npx;
-        stats->reflect_rays = seg - npx;
-        stats->shadow_rays = sh;
+        stats->reflect_rays = sums[0] - npx;
+        stats->shadow_rays = sums[1];
         float ms = 0.f;
-        if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->ev0, c->ev1);
+        if (e == hipSuccess && npx) e = hipEventElapsedTime(&ms, c->ev0, c->ev1);
         stats->kernel_ms = ms;
     }
-    cleanup();
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render: ") + hipGetErrorString(e));
     return RT_OK;
 }
@@ -859,6 +927,7 @@ extern "C" int rt_diag_tile_order(rt_ctx* c, int mode) {
     if (!c || (mode != 0 && mode != 1)) return rt_fail(RT_EINVAL, "rt_diag_tile_order: bad args");
     c->order_mode = mode;
     c->order_valid = false;
+    c->seen_valid = false;
     return RT_OK;
 }
 

@@ -161,3 +161,20 @@ def test_errors_on_bad_host_args():
     assert L.rt_set_scene(None, None) == abi.RT_EINVAL
     assert L.rt_diag_tile_order(None, 0) == abi.RT_EINVAL
     assert L.rt_render_dev(None, None, 8, 8, 1, None, None, None, None, None, None) == abi.RT_EINVAL
+
+
+@pytest.mark.parametrize("H,n,hb", [(1080, 8, 0), (2160, 8, 0), (1080, 7, 0), (133, 3, 5), (5, 8, 0), (4320, 2, 0),
+                                    (1, 1, 0)])
+def test_band_plan_matches_host_plan(H, n, hb):
+    """rt_band_plan (the C-ABI group's row split) agrees with the Python BandPlan and rt_local_rows."""
+    from ray_tracer_fragment_shader_amd.distributed import BandPlan
+    L = abi.lib()
+    band, slab = ctypes.c_int(), ctypes.c_int()
+    abi.check(L.rt_band_plan(H, n, hb, ctypes.byref(band), ctypes.byref(slab)), "rt_band_plan")
+    plan = BandPlan(H, n, hb or None)
+    assert band.value == plan.band_height
+    assert slab.value == plan.slab_rows
+    assert sum(plan.frame_local) == H
+    if H == 2160 and n == 8:
+        assert band.value == 15 and plan.balanced
+    assert L.rt_band_plan(H, 0, 0, ctypes.byref(band), None) == abi.RT_EINVAL
