@@ -114,31 +114,6 @@ int setup_root_events(rt_group* g) {
 
 }  // namespace
 
-extern "C" int rt_band_plan(int height, int n_ranks, int band_height, int* band_out, int* slab_rows_out) {
-    if (height <= 0 || n_ranks <= 0 || band_height < 0 || !band_out)
-        return rt_fail(RT_EINVAL, "rt_band_plan: bad arguments");
-    int hb = band_height;
-    if (hb == 0) {
-        // Largest band height <= 16 giving every rank the same rows (e.g. 15 for 1080 rows over 8 ranks);
-        // 8 when no such height exists (ranks then differ by at most one band).
-        hb = 8;
-        for (int h = 16; h >= 1; --h)
-            if (height % (h * n_ranks) == 0) { hb = h; break; }
-    }
-    if (n_ranks == 1) hb = std::max(hb, 1);
-    int slab = 0;
-    for (int q = 0; q < n_ranks; ++q) {
-        rt_rows r = {hb, n_ranks, q, 1};
-        int nl = 0;
-        int rc = rt_local_rows(height, &r, &nl);
-        if (rc) return rc;
-        slab = std::max(slab, nl);
-    }
-    *band_out = hb;
-    if (slab_rows_out) *slab_rows_out = slab;
-    return RT_OK;
-}
-
 extern "C" int rt_comm_unique_id(uint8_t* id) {
     if (!id) return rt_fail(RT_EINVAL, "rt_comm_unique_id: null id");
     static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "RCCL unique id size");

@@ -232,6 +232,32 @@ extern "C" int rt_global_row(int height, const rt_rows* r, int local_row, int* o
     return RT_OK;
 }
 
+// Row bands of the multi-GPU group (rt_group.cpp).
+extern "C" int rt_band_plan(int height, int n_ranks, int band_height, int* band_out, int* slab_rows_out) {
+    if (height <= 0 || n_ranks <= 0 || band_height < 0 || !band_out)
+        return rt_fail(RT_EINVAL, "rt_band_plan: bad arguments");
+    int hb = band_height;
+    if (hb == 0) {
+        // Largest band height <= 16 giving every rank the same rows (e.g. 15 for 1080 rows over 8 ranks);
+        // 8 when no such height exists (ranks then differ by at most one band).
+        hb = 8;
+        for (int h = 16; h >= 1; --h)
+            if (height % (h * n_ranks) == 0) { hb = h; break; }
+    }
+    if (n_ranks == 1) hb = std::max(hb, 1);
+    int slab = 0;
+    for (int q = 0; q < n_ranks; ++q) {
+        rt_rows r = {hb, n_ranks, q, 1};
+        int nl = 0;
+        int rc = rt_local_rows(height, &r, &nl);
+        if (rc) return rc;
+        slab = std::max(slab, nl);
+    }
+    *band_out = hb;
+    if (slab_rows_out) *slab_rows_out = slab;
+    return RT_OK;
+}
+
 void rt_camera_basis(const rt_camera* cam, double right[3], double upp[3]) {
     HP ld = hp(cam->look_at) - hp(cam->eye);                                    // :1270
     HP r = normalize(cross(ld, hp(cam->up)));                                   // :1271-1273

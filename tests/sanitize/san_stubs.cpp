@@ -1,0 +1,90 @@
+// san_stubs.cpp — TEST INFRASTRUCTURE for the host sanitizer leg (tests/test_sanitize.py).
+//
+// The host-side sources of the product (csrc/rt_host.cpp, csrc/rt_screen.cpp) run all of the path's host
+// index arithmetic: scene flattening, row bands, the speculative rayTraceScreen chain.  Built here with
+// AddressSanitizer + UndefinedBehaviorSanitizer on the CPU (GPU sanitizers are not available), they need the
+// few HIP runtime calls and the two device entry points rt_screen.cpp makes.  This file supplies host-memory
+// test doubles of those: HIP allocations are malloc/free, copies are memcpy, and rt_trace_rays_dev traces the
+// rays with the oracle's C restatement (oracle/rt_oracle.c).  Never linked into the product library.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "../../ray_tracer_fragment_shader_amd/csrc/rt_internal.hpp"
+
+extern "C" int oracle_trace_rays(const rt_scene* d, const double* starts, const double* ends, int n, int depth,
+                                 double* rgb, uint32_t* raycount, int nthreads);
+
+extern "C" {
+const char* hipGetErrorString(hipError_t) { return "stub"; }
+hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) {
+    *s = reinterpret_cast<hipStream_t>(new int(0));
+    return hipSuccess;
+}
+hipError_t hipStreamDestroy(hipStream_t s) {
+    delete reinterpret_cast<int*>(s);
+    return hipSuccess;
+}
+hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipMalloc(void** p, size_t n) {
+    *p = std::malloc(n);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipHostMalloc(void** p, size_t n, unsigned int) { return hipMalloc(p, n); }
+hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned int) {
+    *d = h;
+    return hipSuccess;
+}
+hipError_t hipFree(void* p) {
+    std::free(p);
+    return hipSuccess;
+}
+hipError_t hipHostFree(void* p) {
+    std::free(p);
+    return hipSuccess;
+}
+hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) {
+    std::memcpy(d, s, n);
+    return hipSuccess;
+}
+}
+
+// A context that keeps a deep copy of the scene (what rt_set_scene uploads) for the oracle to trace.
+struct rt_ctx {
+    rt_scene scene;
+    std::vector<rt_sphere> spheres;
+    std::vector<rt_light> lights;
+    std::vector<rt_mesh> meshes;
+    std::vector<unsigned char> blob;
+};
+
+extern "C" int rt_ctx_create(int, rt_ctx** out) {
+    *out = new rt_ctx();
+    return RT_OK;
+}
+extern "C" int rt_ctx_destroy(rt_ctx* c) {
+    delete c;
+    return RT_OK;
+}
+extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* s) {
+    if (!c) return rt_fail(RT_EINVAL, "rt_set_scene: null context");
+    int rc = rt_build_dev_scene(s, &c->blob);                 // the product's validation + flattening
+    if (rc) return rc;
+    c->scene = *s;
+    c->spheres.assign(s->spheres, s->spheres + s->n_spheres);
+    c->lights.assign(s->lights, s->lights + s->n_lights);
+    c->meshes.assign(s->meshes, s->meshes + s->n_meshes);
+    c->scene.spheres = c->spheres.data();
+    c->scene.lights = c->lights.data();
+    c->scene.meshes = c->meshes.data();
+    return RT_OK;
+}
+extern "C" int rt_trace_rays_dev(rt_ctx* c, const double* starts, const double* ends, int n, int depth,
+                                 double* rgb64f, uint32_t* raycount, void*) {
+    if (!c) return rt_fail(RT_EINVAL, "rt_trace_rays_dev: null context");
+    return oracle_trace_rays(&c->scene, starts, ends, n, depth, rgb64f, raycount, 1);
+}
