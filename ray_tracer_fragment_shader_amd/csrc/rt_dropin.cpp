@@ -42,8 +42,7 @@ static vector<uint8_t> g_rgba;                          // the last frame, botto
 
 void loadScene()                                        // MSA:1495 — same boardMap, now flattened
 {
-   vector<const char*> sq;
-   vector<int32_t> ty;
+   vector<const char*> sq; vector<int32_t> ty;
    for (auto& kv : boardMap) { sq.push_back(kv.first.c_str()); ty.push_back(kv.second); }
    int rc = rt_load_scene(sq.data(), ty.data(), (int)sq.size(), &g_rtScene, g_rtSpheres, RT_MAX_SPHERES,
                           g_rtMeshes, RT_MAX_MESHES, &g_rtLight);

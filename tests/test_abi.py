@@ -178,3 +178,17 @@ def test_band_plan_matches_host_plan(H, n, hb):
     if H == 2160 and n == 8:
         assert band.value == 15 and plan.balanced
     assert L.rt_band_plan(H, 0, 0, ctypes.byref(band), None) == abi.RT_EINVAL
+
+
+def test_integration_snippet_is_the_built_dropin():
+    """Every code line of INTEGRATION.md's drop-in snippet appears in csrc/rt_dropin.cpp, which the Makefile
+    compiles against rt_api.h (-Werror), so the documented binding cannot drift from the header."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    src = open(os.path.join(ROOT, "ray_tracer_fragment_shader_amd", "csrc", "rt_dropin.cpp")).read()
+    block = doc.split("```cpp", 1)[1].split("```", 1)[0]
+    norm = lambda t: " ".join(t.split("//")[0].split())   # noqa: E731
+    src_lines = {norm(x) for x in src.splitlines()}
+    lines = [norm(x) for x in block.splitlines() if norm(x) and not norm(x).startswith("#include")]
+    assert len(lines) > 20
+    missing = [x for x in lines if x not in src_lines]
+    assert not missing, missing

@@ -177,6 +177,39 @@ def test_group_errors_are_loud(tr):
         other.close()
 
 
+def test_group_create_rank_one_process_per_gpu_path(tr):
+    """The one-process-per-GPU constructor (rt_comm_unique_id + rt_group_create_rank, as bench.py uses under
+    torch.distributed.run) with a one-rank communicator: same gather + assembly, equal to one launch."""
+    L = abi.lib()
+    cfg = scenes.CONFIGS["c2"]
+    W, H = 640, 360
+    uid = (ctypes.c_uint8 * abi.RT_COMM_ID_BYTES)()
+    abi.check(L.rt_comm_unique_id(uid), "rt_comm_unique_id")
+    t = Tracer(0)
+    t.set_scene(cfg.scene())
+    g = ctypes.c_void_p()
+    abi.check(L.rt_group_create_rank(t._ctx, 1, 0, uid, ctypes.byref(g)), "rt_group_create_rank")
+    try:
+        info = [ctypes.c_int() for _ in range(4)]
+        abi.check(L.rt_group_info(g, *[ctypes.byref(x) for x in info]), "rt_group_info")
+        assert [x.value for x in info] == [1, 1, 0, abi.RT_TRANSPORT_RCCL]
+        s = torch.cuda.Stream()
+        o8 = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+        cam = cfg.camera(W, H)
+        for _ in range(3):
+            _multi(g, cam, W, H, cfg.depth, 0, None, o8, s)
+        abi.check(L.rt_group_synchronize(g), "rt_group_synchronize")
+        s.synchronize()
+        tr.set_scene(cfg.scene())
+        want = tr.render(cam, W, H, cfg.depth, rgba32f=False, rgba8=True)["rgba8"]
+        torch.cuda.synchronize()
+        assert torch.equal(o8, want)
+        assert L.rt_group_create_rank(t._ctx, 2, 2, uid, ctypes.byref(ctypes.c_void_p())) == abi.RT_EINVAL
+    finally:
+        L.rt_group_destroy(g)
+        t.close()
+
+
 def _read_ppm(path):
     data = open(path, "rb").read()
     parts = data.split(b"\n", 1)
