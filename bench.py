@@ -62,6 +62,13 @@ def parse():
                     help="skip parity/ray-count/cpu and extra legs (for rocprofv3 runs)")
     ap.add_argument("--no-c4", action="store_true", help="skip the c4 (row split + RCCL gather) leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the c3/c5 and drop-in legs (N = 1)")
+    ap.add_argument("--frames-in-flight", type=int, default=2,
+                    help="independent frames round-robin over this many HIP streams, each with its own context and "
+                         "output buffers, so a frame's launch starts while the previous frame's last waves drain "
+                         "(1: one stream, launches back to back)")
+    ap.add_argument("--settle", type=float, default=0.25,
+                    help="seconds of untimed back-to-back frames before the warm-up steps, so the GPU clock reaches "
+                         "its loaded steady state (MI355X_MICROARCH.md 'DVFS give-back')")
     return ap.parse_args()
 
 
@@ -108,6 +115,50 @@ def kernel_rooflines(cfg_name, nl, W, H, avg_kern_ms):
              "kernel_ms": round(avg_kern_ms, 5), "algorithmic_bytes_per_launch": bytes_launch},
             {"bound": "fp64-valu", "achieved": round(tflops, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
              "frac": round(tflops / FP64_PEAK_TFLOPS, 4), "flops_per_launch": flops_launch})
+
+
+def pipelined_frames(torch, L, abi, trs, sts, launch_args, steps, settle_s):
+    """Untimed settle, then `steps` frames round-robin over the streams `sts` (launch_args[i] on sts[i]).
+    Returns (wall seconds, per-frame interval in ms from HIP events bracketing all streams)."""
+    n = len(launch_args)
+    fn = L.rt_render_dev
+    t_end = time.perf_counter() + settle_s
+    k = 0
+    while time.perf_counter() < t_end or k < 2 * n:
+        for _ in range(16):
+            abi.check(fn(*launch_args[k % n]), "rt_render_dev")
+            k += 1
+        torch.cuda.synchronize()
+    s0 = sts[0]
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(s0)
+    for s in sts[1:]:
+        s.wait_event(ev0)
+    for i in range(steps):
+        rc = fn(*launch_args[i % n])
+        if rc:
+            abi.check(rc, "rt_render_dev")
+    for s in sts[1:]:
+        e = torch.cuda.Event()
+        e.record(s)
+        s0.wait_event(e)
+    ev1.record(s0)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, ev0.elapsed_time(ev1) / steps
+
+
+def serial_kernel_ms(torch, L, abi, launch, stream, n=20):
+    """Average duration of `n` back-to-back launches on one stream (HIP events on that stream)."""
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    torch.cuda.synchronize()
+    e[0].record(stream)
+    for _ in range(n):
+        abi.check(L.rt_render_dev(*launch), "rt_render_dev")
+    e[1].record(stream)
+    torch.cuda.synchronize()
+    return e[0].elapsed_time(e[1]) / n
 
 
 def main() -> int:
@@ -191,7 +242,7 @@ def main() -> int:
             abi.check(L.rt_group_synchronize(g), "rt_group_synchronize")
             torch.cuda.synchronize()
 
-        for _ in range(max(warmup, 3)):                   # includes the tile-order calibration of every rank
+        for _ in range(max(warmup, 20)):                  # includes the tile-order calibration of every rank
             abi.check(fn(*argv), "rt_render_multi")
         sync()
         barrier()
@@ -244,7 +295,8 @@ def main() -> int:
             tr.render_into(cam, W, H, B, bufs, rows=plan.rows(rank))
         e[1].record(stream)
         torch.cuda.synchronize()
-        avg_kern_ms = e[0].elapsed_time(e[1]) / 20
+        avg_kern_ms = kern_serial_ms = e[0].elapsed_time(e[1]) / 20
+        nfly = 1
         parity = f"gathered RGBA8 frame == one-launch frame: {info['parity']}"
         res_extra["group"] = info
     else:
@@ -259,17 +311,6 @@ def main() -> int:
         rows = plan.rows(rank) if streams else None
         nl = plan.local[prank]                 # rows this rank renders per step (all its frames)
         fl = plan.frame_local[prank]           # ... per frame
-        out32 = torch.empty((nl, W, 4), dtype=torch.float32, device=dev)
-        # RGBA8 slabs are double-buffered only where a step's exchange reads them while the next step renders
-        # (frame streams); independent frames write one buffer.
-        out8 = [torch.empty((nl, W, 4), dtype=torch.uint8, device=dev) for _ in range(2 if streams else 1)]
-        out8 = out8 * (2 // len(out8))
-        if streams:
-            recv8 = [torch.empty((world, fl, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
-            image8 = [torch.empty((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
-            side = torch.cuda.Stream(dev)
-            assembled = [torch.cuda.Event() for _ in range(2)]
-            pending = [None, None]
 
         # ---- parity + ray count (outside the timed region) ----------------------------------------------
         rays_frame = scenes.PINNED_RAYS.get(args.config)
@@ -288,24 +329,66 @@ def main() -> int:
             parity = "bit-exact on 4096 sampled pixels vs the reference's rayTraceRay (tests/golden)"
             del chk, rc
 
-        # Pre-bound launches: the ctypes argument tuples are built once, so the timed loop only issues
-        # rt_render_dev (host cost ~8 us per call; the GPU queue stays full).
         fn = L.rt_render_dev
-        rows_ref = ctypes.byref(rows) if rows is not None else None
-        launch_args = [(tr._ctx, ctypes.byref(cam), W, H, B, rows_ref, ctypes.c_void_p(out32.data_ptr()),
-                        ctypes.c_void_p(out8[b].data_ptr()), None, None, ctypes.c_void_p(stream.cuda_stream))
-                       for b in range(2)]
-        counter = [0]
+        if not streams:
+            # Independent frames: frame s goes to stream s % F with its own context and output buffers, so its
+            # launch fills the tail of frame s-1 (F = --frames-in-flight).  Every frame is a full render.
+            nfly = max(1, args.frames_in_flight)
+            trs = [tr] + [Tracer(local) for _ in range(nfly - 1)]
+            for t in trs[1:]:
+                t.set_scene(scene)
+            sts = [stream] + [torch.cuda.Stream(dev) for _ in range(nfly - 1)]
+            outs = [(torch.empty((nl, W, 4), dtype=torch.float32, device=dev),
+                     torch.empty((nl, W, 4), dtype=torch.uint8, device=dev)) for _ in range(nfly)]
+            launch_args = [(trs[i]._ctx, ctypes.byref(cam), W, H, B, None, ctypes.c_void_p(outs[i][0].data_ptr()),
+                            ctypes.c_void_p(outs[i][1].data_ptr()), None, None, ctypes.c_void_p(sts[i].cuda_stream))
+                           for i in range(nfly)]
+            # Setup (untimed): per context, the first render of the view uses the identity tile order, the
+            # second times its tile rows (calibration), later renders dispatch the longest rows first; then
+            # --settle seconds of frames and the --warmup steps, untimed.
+            for _ in range(2):
+                for la in launch_args:
+                    abi.check(fn(*la), "rt_render_dev")
+            torch.cuda.synchronize()
+            wsteps = max(args.warmup, 0)
+            for i in range(wsteps):
+                abi.check(fn(*launch_args[i % nfly]), "rt_render_dev")
+            torch.cuda.synchronize()
+            barrier()
+            elapsed, avg_kern_ms = pipelined_frames(torch, L, abi, trs, sts, launch_args, args.steps, args.settle)
+            barrier()
+            # (skipped in --profile-kernel-only runs, whose trace must end with the timed dispatches)
+            kern_serial_ms = (None if args.profile_kernel_only else
+                              serial_kernel_ms(torch, L, abi, launch_args[0], stream))
+            elapsed = max_over_ranks(elapsed)
+            for t in trs[1:]:
+                t.close()
+        else:
+            out32 = torch.empty((nl, W, 4), dtype=torch.float32, device=dev)
+            # RGBA8 slabs are double-buffered: a step's exchange reads them while the next step renders
+            out8 = [torch.empty((nl, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
+            recv8 = [torch.empty((world, fl, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
+            image8 = [torch.empty((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
+            side = torch.cuda.Stream(dev)
+            assembled = [torch.cuda.Event() for _ in range(2)]
+            pending = [None, None]
+            nfly = 1
+            # Pre-bound launches: the ctypes argument tuples are built once, so the timed loop only issues
+            # rt_render_dev (host cost ~8 us per call; the GPU queue stays full).
+            rows_ref = ctypes.byref(rows)
+            launch_args = [(tr._ctx, ctypes.byref(cam), W, H, B, rows_ref, ctypes.c_void_p(out32.data_ptr()),
+                            ctypes.c_void_p(out8[b].data_ptr()), None, None, ctypes.c_void_p(stream.cuda_stream))
+                           for b in range(2)]
+            counter = [0]
 
-        def step():
-            b = counter[0] % 2
-            counter[0] += 1
-            if streams and pending[b] is not None:
-                pending[b].wait()                               # the all-to-all of step s-2 has read out8[b]
-            rc = fn(*launch_args[b])
-            if rc:
-                abi.check(rc, "rt_render_dev")
-            if streams:
+            def step():
+                b = counter[0] % 2
+                counter[0] += 1
+                if pending[b] is not None:
+                    pending[b].wait()                           # the all-to-all of step s-2 has read out8[b]
+                rc = fn(*launch_args[b])
+                if rc:
+                    abi.check(rc, "rt_render_dev")
                 stream.wait_event(assembled[b])                 # recv8[b] consumed by the assembly of step s-2
                 pending[b] = exchange_frames(out8[b].view(world, fl, W, 4), recv8[b], world, async_op=True)
                 with torch.cuda.stream(side):
@@ -316,47 +399,33 @@ def main() -> int:
                     assemble_on_device(recv8[b], plan, W, image8[b], side)
                     assembled[b].record(side)
 
-        # Setup (untimed, independent of --warmup): the first render of a view uses the identity tile order,
-        # the second times its tile rows (calibration), later renders dispatch the longest rows first.
-        for _ in range(2):
-            for la in launch_args:
-                abi.check(fn(*la), "rt_render_dev")
-        torch.cuda.synchronize()
-        for _ in range(args.warmup):
-            step()
-        barrier()
-        torch.cuda.synchronize()
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for _ in range(args.steps):
-            step()
-        ev1.record(stream)
-        torch.cuda.synchronize()                                # every stream: render, exchange, assembly
-        barrier()
-        elapsed = time.perf_counter() - t0
-        if not streams:
-            # HIP events on the launch stream bracketing the timed region, which holds only the K launches of
-            # rt_render_kernel (per-launch event pairs would serialise the queue and add ~8 us per launch).
-            avg_kern_ms = ev0.elapsed_time(ev1) / args.steps
-        else:
+            for _ in range(2):
+                for la in launch_args:
+                    abi.check(fn(*la), "rt_render_dev")
+            torch.cuda.synchronize()
+            for _ in range(args.warmup):
+                step()
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()                            # every stream: render, exchange, assembly
+            barrier()
+            elapsed = time.perf_counter() - t0
             # the timed region also holds the exchange: time the kernel alone in a short post-pass
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            n = min(args.steps, 20)
-            torch.cuda.synchronize()
-            e[0].record(stream)
-            for _ in range(n):
-                fn(*launch_args[0])
-            e[1].record(stream)
-            torch.cuda.synchronize()
-            avg_kern_ms = e[0].elapsed_time(e[1]) / n
-        elapsed = max_over_ranks(elapsed)
+            avg_kern_ms = kern_serial_ms = serial_kernel_ms(torch, L, abi, launch_args[0], stream)
+            elapsed = max_over_ranks(elapsed)
 
     rays_step = rays_frame * job_frames
     value = rays_step * args.steps / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
     roof, roof64 = kernel_rooflines(args.config, nl, W, H, avg_kern_ms)
+    roof["kernel_ms_serial"] = round(kern_serial_ms, 5) if kern_serial_ms is not None else None
+    roof["frames_in_flight"] = nfly
+    roof["kernel_ms_note"] = ("kernel_ms: per-frame interval of rt_render_kernel over the timed region, HIP events "
+                              f"bracketing the {nfly} launch stream(s) (a frame's launch overlaps the previous "
+                              "frame's tail when > 1); kernel_ms_serial: launches back to back on one stream")
     if world > 1:
         roof["traffic"] = None                               # the PMC figures are whole-frame, one GPU
 
@@ -376,7 +445,7 @@ def main() -> int:
 
     if rank == 0 and world == 1 and extra_ok and not args.no_extra:
         confs = {}
-        for name, k in (("c3", 30), ("c5", 10)):
+        for name, k in (("c3", 40), ("c5", 16)):
             c = scenes.CONFIGS[name]
             t = Tracer(local)
             t.set_scene(c.scene())
@@ -384,24 +453,29 @@ def main() -> int:
             rays = frame_rays(t, cc, c.width, c.height, c.depth)
             if rays != scenes.PINNED_RAYS[name]:
                 raise SystemExit(f"{name}: ray count {rays} != reference {scenes.PINNED_RAYS[name]}")
-            bufs = t.alloc(c.width, c.height, rgba32f=True, rgba8=True)
-            for _ in range(3):
-                t.render_into(cc, c.width, c.height, c.depth, bufs)
-            torch.cuda.synchronize()
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            t0c = time.perf_counter()
-            e[0].record(stream)
-            for _ in range(k):
-                t.render_into(cc, c.width, c.height, c.depth, bufs)
-            e[1].record(stream)
-            torch.cuda.synchronize()
-            wall = (time.perf_counter() - t0c) / k
-            kms = e[0].elapsed_time(e[1]) / k
+            nf = max(1, args.frames_in_flight)
+            ts = [t] + [Tracer(local) for _ in range(nf - 1)]
+            for tt in ts[1:]:
+                tt.set_scene(c.scene())
+            ss = [stream] + [torch.cuda.Stream(dev) for _ in range(nf - 1)]
+            bb = [tt.alloc(c.width, c.height, rgba32f=True, rgba8=True) for tt in ts]
+            la = [(ts[i]._ctx, ctypes.byref(cc), c.width, c.height, c.depth, None,
+                   ctypes.c_void_p(bb[i]["rgba32f"].data_ptr()), ctypes.c_void_p(bb[i]["rgba8"].data_ptr()), None,
+                   None, ctypes.c_void_p(ss[i].cuda_stream)) for i in range(nf)]
+            for _ in range(2):
+                for a in la:
+                    abi.check(L.rt_render_dev(*a), "rt_render_dev")
+            wall, kms = pipelined_frames(torch, L, abi, ts, ss, la, k, min(args.settle, 0.1))
+            wall /= k
+            kser = serial_kernel_ms(torch, L, abi, la[0], stream, n=max(5, k // 2))
+            for tt in ts[1:]:
+                tt.close()
             r1, r2 = kernel_rooflines(name, c.height, c.width, c.height, kms)
             confs[name] = {"workload": f"{name}: {c.width}x{c.height}, {c.n_spheres} spheres + board, "
                                        f"{c.n_lights} light(s), {c.depth} bounce(s), one GPU",
                            "ms_per_frame": round(wall * 1e3, 4), "value": round(rays / wall / 1e6, 3),
                            "unit": "Mray/s", "rays_per_frame": rays, "kernel_ms": round(kms, 5),
+                           "kernel_ms_serial": round(kser, 5), "frames_in_flight": nf,
                            "hbm_frac": r1["frac"], "hbm_traffic": r1["traffic"],
                            "algorithmic_bytes": r1["algorithmic_bytes_per_launch"], "fp64_frac": r2["frac"]}
             t.close()

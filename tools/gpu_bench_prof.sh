@@ -16,5 +16,5 @@ for c in ${CONFIGS:-c2 c3 c5}; do
       python3 "$ROOT/bench.py" --config $c --steps $steps --warmup 5 --no-cpu-baseline --profile-kernel-only \
       > "$OUT/prof_bench_$c.json" 2> "$OUT/prof_$c.err" || { echo "rocprof $c failed"; tail -20 "$OUT/prof_$c.err"; exit 4; }
   echo "== $c"; find "$OUT/prof_$c" -name "*kernel_stats.csv" -exec head -3 {} \;
-  (cd "$ROOT" && python3 tools/kernel_gaps.py "$OUT/prof_$c" | tee "$OUT/prof_dispatches_$c.json")
+  (cd "$ROOT" && python3 tools/kernel_gaps.py "$OUT/prof_$c" $steps | tee "$OUT/prof_dispatches_$c.json")
 done
