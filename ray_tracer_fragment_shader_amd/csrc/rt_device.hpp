@@ -51,6 +51,11 @@
 #ifndef RT_UNIFORM_SHADOW
 #define RT_UNIFORM_SHADOW 0
 #endif
+// 1: the fast (non-CULL) bounce loop keeps the continuation's unit direction live through the light loop;
+// 0: it is recomputed after it (fewer live registers).
+#ifndef RT_KEEP_NU
+#define RT_KEEP_NU 0
+#endif
 
 namespace rt {
 
@@ -924,28 +929,40 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
 // mslot[k kSlotStride], component-major so a wave's 64 lanes touch 64 consecutive words.
 constexpr int kSlotStride = 256;
 
-// A hit at level lvl: park its colour in LDS and turn r into the continuation ray (:1238-1247).
-template <int B, bool TRANSP, int SS = kSlotStride>
-__device__ __forceinline__ void continue_ray(const SceneView& V, int lvl, int kind, int mat, d3 p, d3 n, d3 rd,
-                                             d3 rdir, d3 c, Ray* r, int* levels, uint32_t* nsh, double* slot,
-                                             int* mslot) {
-    const DevScene* S = V.S;
+// The continuation of a hit at level lvl (:1238-1247), computed before the light loop: its end - start
+// (the transmitted ray's when the material transmits, else the reflected ray's rd) and the material id.
+template <bool TRANSP>
+__device__ __forceinline__ d3 continuation(const SceneView& V, int kind, int mat, d3 p, d3 n, d3 u, d3 rd) {
+    if (TRANSP && V.S->mat[mat].transmit) return sub(transmitted_end(V, kind, mat, p, u, n), p);   // Line(p, p + t)
+    return rd;                                                                                       // Line(p, p + r)
+}
+
+// A hit at level lvl: park its colour (and, TRANSP, its material for the weight w) in LDS.
+template <bool TRANSP, int SS = kSlotStride>
+__device__ __forceinline__ void park_level(int lvl, int mat, d3 c, double* slot, int* mslot) {
     double* sl = slot + 3 * lvl * SS;
     sl[0] = c.x;
     sl[SS] = c.y;
     sl[2 * SS] = c.z;
-    *nsh += V.nl;
-    *levels = lvl + 1;
-    if (TRANSP && S->mat[mat].transmit) {
-        d3 pt = transmitted_end(V, kind, mat, p, r->u, n);
-        d3 td = sub(pt, p);                                 // transmittedRay = Line(p, p + t)
-        r->p0 = p;                                          // the next level traces the continuation
-        set_dir(r, td, unit(td));
-    } else {
-        r->p0 = p;
-        set_dir(r, rd, rdir);
-    }
     if (TRANSP) mslot[lvl * SS] = mat;
+}
+
+// The next level's ray for EVERY lane: Line(p, p + nd) for lanes that hit; lanes that did not get a zero
+// ray (they are not alive at the next level and never trace it).  Assigning it unconditionally ends the
+// live range of the previous ray at the hit test, so it is not carried through the light loop (the
+// compiler cannot see that a lane which did not hit never reads its ray again).  u = unit(nd) is
+// recomputed here (same operations, same bits) rather than kept live through the light loop.
+__device__ __forceinline__ void next_ray(bool hit, d3 p, d3 nd, Ray* r) {
+    d3 nu = nd;
+    if (hit) nu = unit(nd);                                 // not for the zero rays: unit(0) is the slow path
+    r->p0 = p;
+    set_dir(r, nd, nu);
+}
+
+// As above with the continuation's unit direction kept from before the light loop (RT_KEEP_NU).
+__device__ __forceinline__ void next_ray(d3 p, d3 nd, d3 nu, Ray* r) {
+    r->p0 = p;
+    set_dir(r, nd, nu);
 }
 
 // One bounce level of the CULL variant, run by all lanes of the wave (ray_bundle_mask and shade's
@@ -967,17 +984,23 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     }
     const bool hit = kind >= 0;
     if (!__any(hit)) return false;
-    d3 n = mk(0.0, 0.0, 0.0), pe = n, rd = n;
+    d3 n = mk(0.0, 0.0, 0.0), nd = n;
     int mat = 0;
     double ks = 0.0;
     if (hit) {
+        d3 pe;
         surface(V, kind, p, r->u, &n, &mat, &pe);
-        rd = sub(pe, p);                                    // reflectedRay = Line(p, p + r)
+        const d3 rd = sub(pe, p);                           // reflectedRay = Line(p, p + r)
         ks = fabs(dot(r->u, unit(rd)));                     // |u . reflectedRay.direction()|
+        nd = continuation<TRANSP>(V, kind, mat, p, n, r->u, rd);
     }
     const d3 c = shade<TRANSP, true>(V, hit, p, n, mat, ks);
-    // rdir is recomputed (same operations, same bits) rather than kept live through the light loop.
-    if (hit) continue_ray<B, TRANSP, SS>(V, lvl, kind, mat, p, n, rd, unit(rd), c, r, levels, nsh, slot, mslot);
+    if (hit) {
+        park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
+        *nsh += V.nl;
+        *levels = lvl + 1;
+    }
+    if (lvl < B) next_ray(hit, p, nd, r);
     return true;
 }
 
@@ -999,25 +1022,44 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
         if (CULL) {
             if (!cull_level<B, TRANSP, SS>(V, lvl, first, alive, bdP, bdd, cone, &r, &levels, &nseg, &nsh, slot, mslot))
                 break;
-        } else if (alive) {
-            ++nseg;
-            d3 p;
-            int kind;
-            if (first) {
-                kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p);
-            } else {
-                set_origin_f32(S, &r);
-                kind = closest_hit<TRANSP>(V, r, &p);
+        } else {
+            d3 p = mk(0.0, 0.0, 0.0);
+            int kind = -1;
+            if (alive) {
+                ++nseg;
+                if (first) {
+                    kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p);
+                } else {
+                    set_origin_f32(S, &r);
+                    kind = closest_hit<TRANSP>(V, r, &p);
+                }
             }
-            if (kind >= 0) {
+            const bool hit = kind >= 0;
+            d3 nd = mk(0.0, 0.0, 0.0);
+#if RT_KEEP_NU
+            d3 nu = nd;
+#endif
+            if (hit) {
                 d3 n, pe;
                 int mat;
                 surface(V, kind, p, r.u, &n, &mat, &pe);
-                d3 rd = sub(pe, p);                         // reflectedRay = Line(p, p + r)
-                d3 rdir = unit(rd);                         // reflectedRay.direction()
-                const d3 c = shade<TRANSP, false>(V, true, p, n, mat, fabs(dot(r.u, rdir)));
-                continue_ray<B, TRANSP, SS>(V, lvl, kind, mat, p, n, rd, rdir, c, &r, &levels, &nsh, slot, mslot);
+                const d3 rd = sub(pe, p);                   // reflectedRay = Line(p, p + r)
+                const d3 rdir = unit(rd);                   // reflectedRay.direction()
+                const double ks = fabs(dot(r.u, rdir));     // |u . reflectedRay.direction()|
+                nd = continuation<TRANSP>(V, kind, mat, p, n, r.u, rd);
+#if RT_KEEP_NU
+                nu = (TRANSP && V.S->mat[mat].transmit) ? unit(nd) : rdir;
+#endif
+                const d3 c = shade<TRANSP, false>(V, true, p, n, mat, ks);
+                park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
+                nsh += V.nl;
+                levels = lvl + 1;
             }
+#if RT_KEEP_NU
+            if (lvl < B) next_ray(p, nd, nu, &r);
+#else
+            if (lvl < B) next_ray(hit, p, nd, &r);
+#endif
         }
     }
     d3 acc = mk(0.0, 0.0, 0.0);

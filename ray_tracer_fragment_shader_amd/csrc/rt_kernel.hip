@@ -37,9 +37,11 @@ using namespace rt;
 #ifndef RT_WAVE_TRACE
 #define RT_WAVE_TRACE 0
 #endif
-// __launch_bounds__ minimum waves per EU of the depth <= 3 render kernels (5: <= 96 VGPRs).
+// __launch_bounds__ minimum waves per EU of the depth <= 3 render kernels.  0 (default): 6 for depth <= 2
+// (<= 80 VGPRs, no spills since the bounce loop stopped carrying the previous ray through the light loop),
+// 5 for depth 3 (<= 96 VGPRs; 6 would spill 8 B/lane).
 #ifndef RT_MINW
-#define RT_MINW 5
+#define RT_MINW 0
 #endif
 #ifndef RT_NT_STORES
 #define RT_NT_STORES 0                         // 1: non-temporal RGBA32F/RGBA8 stores (A/B)
@@ -48,7 +50,7 @@ using namespace rt;
 #define RT_WG_FAST 64                          // workgroup of the default render kernels: 64 (8 x 8) or 128 (16 x 8)
 #endif
 #ifndef RT_MINW_CULL
-#define RT_MINW_CULL RT_MINW                   // the culling variant (>= kConeMin spheres)
+#define RT_MINW_CULL 5                         // the culling variant (>= kConeMin spheres): 87 VGPRs, no spills
 #endif
 
 namespace {
@@ -468,25 +470,39 @@ __global__ __launch_bounds__(kThreads) void rt_probe_math_kernel(int op, const d
 
 // ------------------------------------------------------------------------------------------------
 // Template dispatch.
+// RT_MAX_B < 7 (experiment builds only, tools/variants.sh): deeper kernels are not instantiated.
+#ifndef RT_MAX_B
+#define RT_MAX_B 7
+#endif
+// MINW = 0: the depth-dependent default of RT_MINW (6 for depth <= 2, else 5).
+template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG>
+hipError_t launch_render_one(dim3 grid, size_t lds, hipStream_t st, const DevScene* s, const RenderParams& P,
+                             float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
+    constexpr int MW = MINW != 0 ? MINW : (B <= 2 ? 6 : 5);
+    if constexpr (B > RT_MAX_B) {
+        return hipErrorInvalidValue;
+    } else {
+        if (lds > 65536) {
+            hipError_t e = hipFuncSetAttribute((const void*)rt_render_kernel<B, LDS, MW, TRANSP, CULL, WG>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL((rt_render_kernel<B, LDS, MW, TRANSP, CULL, WG>), grid, dim3(WG), lds, st, s, P, o32, o8,
+                           o64, orc);
+        return hipGetLastError();
+    }
+}
+
 template <int LDS, int MINW, bool TRANSP, bool CULL = false, int WG = kThreads>
 hipError_t launch_render_lds(int depth, dim3 grid, size_t lds, hipStream_t st, const DevScene* s,
                              const RenderParams& P, float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
-#define RT_CASE(b)                                                                                      \
-    case b:                                                                                             \
-        if (lds > 65536) {                                                                              \
-            hipError_t e_ = hipFuncSetAttribute((const void*)rt_render_kernel<b, LDS, MINW, TRANSP, CULL, WG>,                  \
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);  \
-            if (e_ != hipSuccess) return e_;                                                            \
-        }                                                                                               \
-        hipLaunchKernelGGL((rt_render_kernel<b, LDS, MINW, TRANSP, CULL, WG>), grid, dim3(WG), lds, st, s, P, o32, o8,    \
-                           o64, orc);                                                                   \
-        break;
+#define RT_CASE(b) \
+    case b: return launch_render_one<b, LDS, MINW, TRANSP, CULL, WG>(grid, lds, st, s, P, o32, o8, o64, orc);
     switch (depth) {
         RT_CASE(0) RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7)
         default: return hipErrorInvalidValue;
     }
 #undef RT_CASE
-    return hipGetLastError();
 }
 
 template <bool TRANSP>
@@ -525,8 +541,8 @@ struct rt_ctx {
                                                // the per-eye data, so every later render re-prepares it
     double eye[3] = {0, 0, 0};
     std::vector<unsigned char> blob;           // host image of d_scene (rt_set_scene skips an unchanged scene)
-    int min_waves = 5;                         // __launch_bounds__(256, 5) for depth <= 3 (measured faster
-                                               // despite small spills: tools/ab.py); RT_MIN_WAVES=0 disables
+    int min_waves = 5;                         // >= 5: the RT_MINW / RT_MINW_CULL launch bounds for depth <= 3 (measured faster
+                                               // than no bound: tools/ab.py); RT_MIN_WAVES=0 disables
     int use_lds = 0;                           // RT_SCENE_IN_LDS=1: header + exact records in LDS (A/B: tools/ab.py)
     int wg_staging = 0;                        // RT_WG_STAGING=1: LDS-staged 32-pixel row stores (A/B)
     // Adaptive tile-row order (rt_order_kernel): the first render of a new (scene, camera, size, rows,
