@@ -44,7 +44,7 @@ extern "C" {
 #define RT_EINVAL       -1   /* bad argument (null pointer, size, unsupported material, ...) */
 #define RT_EHIP         -2   /* HIP runtime error or no device */
 #define RT_ENOMEM       -3   /* allocation failed */
-#define RT_EUNSUPPORTED -4   /* reference feature outside the GPU path (cylinder/cone stubs, branching rays) */
+#define RT_EUNSUPPORTED -4   /* reference feature outside the GPU path (cylinder/cone stubs) */
 
 #define RT_MAX_SPHERES 1024
 #define RT_MAX_LIGHTS  16

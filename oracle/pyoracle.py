@@ -90,6 +90,10 @@ def ref() -> ctypes.CDLL:
                                     c_void_p, c_void_p, c_void_p]
         L.ref_convert_string_coordinate.restype = None
         L.ref_convert_string_coordinate.argtypes = [c_char_p, c_void_p]
+        L.ref_set_materials.restype = None
+        L.ref_set_materials.argtypes = [c_void_p]
+        L.ref_default_materials.restype = None
+        L.ref_default_materials.argtypes = [c_void_p]
         L.ref_screen_rand_calls.restype = c_uint64
         L.ref_screen_rand_calls.argtypes = scene_args + [c_int, c_int, c_int, c_int, ctypes.c_uint, c_uint64]
         _ref = L
@@ -205,14 +209,30 @@ def ref_screen_rand_calls(scene, width, height, bottom_x=None, bottom_y=None, se
     """rand() calls made by the reference's own rayTraceScreen on this frame (glibc rand, MAX_DEPTH)."""
     bx = -(width // 2) if bottom_x is None else bottom_x
     by = -(height // 2) if bottom_y is None else bottom_y
-    return int(ref().ref_screen_rand_calls(*scene.ref_args(), width, height, bx, by, seed, max_calls))
+    return int(_ref_scene(scene).ref_screen_rand_calls(*scene.ref_args(), width, height, bx, by, seed, max_calls))
 
 
 # ------------------------------------------------------------------------------------- reference build
+def _ref_scene(scene):
+    """The reference library with its five material globals set to the scene's (every ref_* call: the
+    scenes it builds copy them), -> the library."""
+    L = ref()
+    m = np.ascontiguousarray(scene.material_values(), np.float64)
+    L.ref_set_materials(_ptr(m))
+    return L
+
+
+def ref_materials():
+    """The reference's own material globals (5 x 13 doubles) as it initialised them (MSA:583-588)."""
+    m = np.zeros(65, np.float64)
+    ref().ref_default_materials(_ptr(m))
+    return m
+
+
 def ref_render(scene, width, height, depth, pitch, row_begin=0, row_end=None, nthreads=0):
     row_end = height if row_end is None else row_end
     rgb = np.zeros((row_end - row_begin, width, 3), np.float64)
-    ref().ref_render(*scene.ref_args(), width, height, depth, float(pitch), row_begin, row_end, _ptr(rgb),
+    _ref_scene(scene).ref_render(*scene.ref_args(), width, height, depth, float(pitch), row_begin, row_end, _ptr(rgb),
                      nthreads)
     return rgb
 
@@ -221,7 +241,7 @@ def ref_render_pixels(scene, width, height, depth, pitch, pi, pj, nthreads=0):
     pi = np.ascontiguousarray(pi, np.int32)
     pj = np.ascontiguousarray(pj, np.int32)
     rgb = np.zeros((pi.shape[0], 3), np.float64)
-    ref().ref_render_pixels(*scene.ref_args(), width, height, depth, float(pitch), _ptr(pi), _ptr(pj),
+    _ref_scene(scene).ref_render_pixels(*scene.ref_args(), width, height, depth, float(pitch), _ptr(pi), _ptr(pj),
                             pi.shape[0], _ptr(rgb), nthreads)
     return rgb
 
@@ -230,7 +250,7 @@ def ref_trace_rays(scene, starts, ends, depth):
     starts = np.ascontiguousarray(starts, np.float64)
     ends = np.ascontiguousarray(ends, np.float64)
     rgb = np.zeros((starts.shape[0], 3), np.float64)
-    ref().ref_trace_rays(*scene.ref_args(), _ptr(starts), _ptr(ends), starts.shape[0], depth, _ptr(rgb))
+    _ref_scene(scene).ref_trace_rays(*scene.ref_args(), _ptr(starts), _ptr(ends), starts.shape[0], depth, _ptr(rgb))
     return rgb
 
 
@@ -242,7 +262,7 @@ def ref_intersect(scene, starts, ends):
     hit = np.zeros(n, np.int32)
     mat = np.zeros(n, np.int32)
     a = scene.ref_args()
-    ref().ref_intersect(a[0], a[1], a[2], a[3], a[4], _ptr(starts), _ptr(ends), n, _ptr(out12), _ptr(hit),
+    _ref_scene(scene).ref_intersect(a[0], a[1], a[2], a[3], a[4], _ptr(starts), _ptr(ends), n, _ptr(out12), _ptr(hit),
                         _ptr(mat))
     return {"point": out12[:, 0:3], "normal": out12[:, 3:6], "reflected_end": out12[:, 6:9],
             "transmitted_end": out12[:, 9:12], "hit": hit, "material": mat}

@@ -184,6 +184,41 @@ uint64_t ref_screen_rand_calls(const char* children, int n_children, const doubl
     return ~0ull;
 }
 
+// The five material globals the scene classes copy at construction (:583-588): g_whiteSquare, g_blackSquare,
+// g_sphereMaterial, g_tetrahedronMaterial, g_cubeMaterial; 13 doubles each (ambient, diffuse, specular,
+// transparency, refraction).  ref_get_materials reads them, ref_set_materials replaces them for the scenes
+// built afterwards (tests of materials the app never uses, e.g. partially transparent ones: ray trees).
+static Material* const g_mats[5] = {&g_whiteSquare, &g_blackSquare, &g_sphereMaterial, &g_tetrahedronMaterial,
+                                    &g_cubeMaterial};
+
+void ref_get_materials(double* m) {
+    for (int k = 0; k < 5; ++k, m += 13) {
+        Material& M = *g_mats[k];
+        Point a = M.ambient(), d = M.diffuse(), s = M.specular(), t = M.transparency();
+        Point* v[4] = {&a, &d, &s, &t};
+        for (int q = 0; q < 4; ++q) {
+            m[3 * q] = v[q]->x(); m[3 * q + 1] = v[q]->y(); m[3 * q + 2] = v[q]->z();
+        }
+        m[12] = M.refraction();
+    }
+}
+
+// The globals as the reference initialised them (snapshot taken at load, after their definitions in this
+// translation unit).
+static struct DefaultMats {
+    double m[65];
+    DefaultMats() { ref_get_materials(m); }
+} g_default_mats;
+
+void ref_default_materials(double* m) {
+    for (int k = 0; k < 65; ++k) m[k] = g_default_mats.m[k];
+}
+
+void ref_set_materials(const double* m) {
+    for (int k = 0; k < 5; ++k, m += 13)
+        *g_mats[k] = Material(Point(m), Point(m + 3), Point(m + 6), Point(m + 9), m[12]);
+}
+
 // convertStringCoordinate (:1326-1346).
 void ref_convert_string_coordinate(const char* sq, double out[3]) {
     Point p = convertStringCoordinate(string(sq, 2));

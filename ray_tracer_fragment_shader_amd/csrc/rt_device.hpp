@@ -916,8 +916,9 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
 }
 
 // rayTraceRay(g_scene, lights, Line(p0, p1), color, B) with color starting at 0 (:1184-1249), as a loop.
-// Every in-scope hit spawns exactly one continuation (host-checked): the reflected ray (opacity != 0) or
-// the transmitted ray (transparency != 0 and |transparency| > eps), weighted by that vector (:1238-1247),
+// Every hit of a non-tree scene spawns exactly one continuation (host-checked; ray trees: trace_tree): the
+// reflected ray (opacity != 0) or the transmitted ray (transparency != 0 and |transparency| > eps), weighted
+// by that vector (:1238-1247),
 // so the colour is the right-nested local[0] + w[0] % (local[1] + w[1] % (...)).  TRANSP = false: all
 // materials opaque, no meshes, w = (1,1,1) (multiplication by 1.0 is exact) and any-hit shadows.
 // PRIMARY: p0 is the camera and V.prim/V.primf hold its per-sphere data; (bdP, bdd) = bc - eye, |.|^2;
@@ -1073,6 +1074,87 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
     *seg = nseg;
     *shadow = nsh;
     return acc;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Ray trees (scenes with a material that both transmits and reflects, :1238-1247): rayTraceRay recurses
+// into the transmitted child, then the reflected child, and adds each child's colour weighted by T and by
+// 1 - T to the node's own colour, in that order.  Depth-first walk with an explicit per-lane node stack
+// (node k = the ray at recursion depth B - k on the current path; dynamically indexed, so it lives in
+// scratch memory — this path is for the rare tree scenes, the single-continuation scenes never run it).
+// A child that misses is skipped: the reference adds w % (0,0,0) = +-0 to a colour that is never -0 (it
+// starts at +0 and only sums), which leaves it unchanged.  General closest_hit for every ray (the primary
+// shortcuts give the same bits), closest-hit shadows (FULL).
+struct TreeNode {
+    d3 p, td, rd;                      // hit point, transmitted and reflected ray (end - start)
+    d3 acc;                            // the node's colour so far: local, then + T % child_T, + (1-T) % child_R
+    int mat;
+    int state;                         // 0: transmitted child next, 1: reflected child next, 2: done
+};
+
+// Trace Line(a, a + d) as node k: closest hit, local colour; false on a miss.
+__device__ __forceinline__ bool tree_eval(const SceneView& V, d3 a, d3 d, TreeNode* node, uint32_t* nseg,
+                                          uint32_t* nsh) {
+    Ray r;
+    r.p0 = a;
+    set_dir(&r, d, unit(d));
+    set_origin_f32(V.S, &r);
+    ++*nseg;
+    d3 p;
+    const int kind = closest_hit<true>(V, r, &p);
+    if (kind < 0) return false;
+    d3 n, pe;
+    int mat;
+    surface(V, kind, p, r.u, &n, &mat, &pe);
+    const d3 rd = sub(pe, p);                               // reflectedRay = Line(p, p + r)
+    const double ks = fabs(dot(r.u, unit(rd)));             // |u . reflectedRay.direction()|
+    node->acc = shade<true, false>(V, true, p, n, mat, ks);
+    *nsh += V.nl;
+    node->p = p;
+    node->rd = rd;
+    node->td = V.S->mat[mat].transmit ? sub(transmitted_end(V, kind, mat, p, r.u, n), p) : mk(0.0, 0.0, 0.0);
+    node->mat = mat;
+    node->state = 0;
+    return true;
+}
+
+template <int B>
+__device__ __forceinline__ d3 trace_tree(const SceneView& V, d3 p0, d3 p1, uint32_t* seg, uint32_t* shadow) {
+    TreeNode st[B + 1];
+    uint32_t nseg = 0, nsh = 0;
+    d3 col = mk(0.0, 0.0, 0.0);
+    if (tree_eval(V, p0, sub(p1, p0), &st[0], &nseg, &nsh)) {
+        int k = 0;
+        for (;;) {
+            TreeNode& f = st[k];
+            if (k < B) {                                    // depth B - k > 0: children (:1230)
+                const DevMat& M = V.S->mat[f.mat];
+                if (f.state == 0) {
+                    f.state = 1;
+                    if (M.transmit && tree_eval(V, f.p, f.td, &st[k + 1], &nseg, &nsh)) {
+                        ++k;
+                        continue;
+                    }
+                }
+                if (f.state == 1) {
+                    f.state = 2;
+                    if (M.reflect && tree_eval(V, f.p, f.rd, &st[k + 1], &nseg, &nsh)) {
+                        ++k;
+                        continue;
+                    }
+                }
+            }
+            if (k == 0) break;
+            TreeNode& pa = st[k - 1];                       // f is pa's child: T (state 1) or R (state 2)
+            const DevMat& PM = V.S->mat[pa.mat];
+            pa.acc = add(pa.acc, had(pa.state == 1 ? ld3(PM.wt) : ld3(PM.wo), f.acc));   // :1241, :1246
+            --k;
+        }
+        col = st[0].acc;
+    }
+    *seg = nseg;
+    *shadow = nsh;
+    return col;
 }
 
 }  // namespace rt

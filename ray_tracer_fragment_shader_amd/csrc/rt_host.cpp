@@ -293,10 +293,12 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     const rt_material* mats[5] = {&s->white_square, &s->black_square, &s->sphere_material, &s->tetrahedron_material,
                                   &s->cube_material};
     // rayTraceRay (:1230-1247) spawns a transmitted ray when transparency != 0 and |transparency| > eps, a
-    // reflected ray when opacity = 1 - transparency != 0.  The GPU loop follows one continuation per hit.
+    // reflected ray when opacity = 1 - transparency != 0.  A material that does both makes every hit on it
+    // a branch of a ray tree: such scenes run the trace_tree kernels (depth-first, per-lane node stack);
+    // the others follow one continuation per hit.
     bool used[5] = {true, true, s->n_spheres > 0, false, false};
     for (int m = 0; m < s->n_meshes; ++m) used[s->meshes[m].kind == RT_MESH_TETRAHEDRON ? 3 : 4] = true;
-    bool any_transparent = false;
+    bool any_transparent = false, tree = false;
     rt::DevMat dm[5];
     memset(dm, 0, sizeof(dm));
     for (int m = 0; m < 5; ++m) {
@@ -306,9 +308,7 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
         bool zeroT = T.x == 0 && T.y == 0 && T.z == 0;
         bool transmit = !zeroT && length(T) > s->small_number;                  // :1238
         bool reflect = !(opacity.x == 0 && opacity.y == 0 && opacity.z == 0);   // :1243
-        if (used[m] && transmit && reflect)
-            return rt_fail(RT_EUNSUPPORTED, "rt_set_scene: a partially transparent material spawns two rays per hit "
-                                            "(a ray tree); the GPU path follows one continuation per hit");
+        if (used[m] && transmit && reflect) tree = true;
         if (used[m] && !zeroT) any_transparent = true;
         for (int q = 0; q < 3; ++q) {
             dm[m].amb[q] = M->ambient[q];
@@ -316,9 +316,12 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
             dm[m].spec[q] = M->specular[q];
         }
         put(dm[m].w, transmit ? T : opacity);
+        put(dm[m].wt, T);
+        put(dm[m].wo, opacity);
         dm[m].refr = M->refraction;
         dm[m].transmit = transmit ? 1 : 0;
         dm[m].transparent = zeroT ? 0 : 1;
+        dm[m].reflect = reflect ? 1 : 0;
     }
 
     const size_t bytes = (size_t)rt::scene_bytes_for(s->n_spheres, s->n_meshes, n_tris, s->n_lights);
@@ -394,6 +397,7 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     }
     for (int m = 0; m < 5; ++m) d->mat[m] = dm[m];
     d->transparent = any_transparent ? 1 : 0;
+    d->tree = tree ? 1 : 0;
     d->n_lights = s->n_lights;
     for (int k = 0; k < s->n_lights; ++k) {
         for (int q = 0; q < 3; ++q) {

@@ -118,7 +118,7 @@ __device__ __forceinline__ unsigned char to_u8(double c) {
 __device__ uint64_t* g_wtrace = nullptr;
 #endif
 
-template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads>
+template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false>
 __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
                                                              RenderParams P, float4* __restrict__ out32,
                                                              uchar4* __restrict__ out8,
@@ -191,7 +191,11 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
     const d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(ic + P.bottom_x), right)),
                       scl(P.pitch * (double)(j + P.bottom_y), upp));
     const d3 bdP = sub(ld3(V.S->bc), eye);                  // bounding-sphere deltaP for p0 = camera
-    const d3 col = trace<B, true, TRANSP, CULL, WG>(V, eye, sp, bdP, dot(bdP, bdP), cone, &seg, &sh, slot, mslot);
+    d3 col;
+    if constexpr (TREE)
+        col = trace_tree<B>(V, eye, sp, &seg, &sh);
+    else
+        col = trace<B, true, TRANSP, CULL, WG>(V, eye, sp, bdP, dot(bdP, bdP), cone, &seg, &sh, slot, mslot);
 
     if (WG != kThreads || !P.wg_staging) {
         // Direct stores: each wave writes its 8 x 8 block as 8 row segments (128 B of RGBA32F each) and
@@ -354,7 +358,7 @@ __global__ __launch_bounds__(kThreads) void rt_scene_init_kernel(DevScene* __res
     }
 }
 
-template <int B, bool TRANSP>
+template <int B, bool TRANSP, bool TREE = false>
 __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene* __restrict__ S,
                                                                  const double* __restrict__ starts,
                                                                  const double* __restrict__ ends, int n,
@@ -367,8 +371,12 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
     const SceneView V = view_of(S, S, S->n_padded, S->n_lights);
     double* slot = reinterpret_cast<double*>(smem) + threadIdx.x;
     int* mslot = reinterpret_cast<int*>(smem + 3 * 8 * (B + 1) * kSlotStride) + threadIdx.x;
-    d3 c = trace<B, false, TRANSP, false>(V, ld3(starts + 3 * kk), ld3(ends + 3 * kk), mk(0.0, 0.0, 0.0), 0.0, ~0ull,
-                                   &seg, &sh, slot, mslot);
+    d3 c;
+    if constexpr (TREE)
+        c = trace_tree<B>(V, ld3(starts + 3 * kk), ld3(ends + 3 * kk), &seg, &sh);
+    else
+        c = trace<B, false, TRANSP, false>(V, ld3(starts + 3 * kk), ld3(ends + 3 * kk), mk(0.0, 0.0, 0.0), 0.0,
+                                           ~0ull, &seg, &sh, slot, mslot);
     if (k >= n) return;
     if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
     if (rc) rc[k] = seg | (sh << 16);
@@ -475,7 +483,7 @@ __global__ __launch_bounds__(kThreads) void rt_probe_math_kernel(int op, const d
 #define RT_MAX_B 7
 #endif
 // MINW = 0: the depth-dependent default of RT_MINW (6 for depth <= 2, else 5).
-template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG>
+template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG, bool TREE>
 hipError_t launch_render_one(dim3 grid, size_t lds, hipStream_t st, const DevScene* s, const RenderParams& P,
                              float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
     constexpr int MW = MINW != 0 ? MINW : (B <= 2 ? 6 : 5);
@@ -483,21 +491,21 @@ hipError_t launch_render_one(dim3 grid, size_t lds, hipStream_t st, const DevSce
         return hipErrorInvalidValue;
     } else {
         if (lds > 65536) {
-            hipError_t e = hipFuncSetAttribute((const void*)rt_render_kernel<B, LDS, MW, TRANSP, CULL, WG>,
+            hipError_t e = hipFuncSetAttribute((const void*)rt_render_kernel<B, LDS, MW, TRANSP, CULL, WG, TREE>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL((rt_render_kernel<B, LDS, MW, TRANSP, CULL, WG>), grid, dim3(WG), lds, st, s, P, o32, o8,
+        hipLaunchKernelGGL((rt_render_kernel<B, LDS, MW, TRANSP, CULL, WG, TREE>), grid, dim3(WG), lds, st, s, P, o32, o8,
                            o64, orc);
         return hipGetLastError();
     }
 }
 
-template <int LDS, int MINW, bool TRANSP, bool CULL = false, int WG = kThreads>
+template <int LDS, int MINW, bool TRANSP, bool CULL = false, int WG = kThreads, bool TREE = false>
 hipError_t launch_render_lds(int depth, dim3 grid, size_t lds, hipStream_t st, const DevScene* s,
                              const RenderParams& P, float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
 #define RT_CASE(b) \
-    case b: return launch_render_one<b, LDS, MINW, TRANSP, CULL, WG>(grid, lds, st, s, P, o32, o8, o64, orc);
+    case b: return launch_render_one<b, LDS, MINW, TRANSP, CULL, WG, TREE>(grid, lds, st, s, P, o32, o8, o64, orc);
     switch (depth) {
         RT_CASE(0) RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7)
         default: return hipErrorInvalidValue;
@@ -505,12 +513,12 @@ hipError_t launch_render_lds(int depth, dim3 grid, size_t lds, hipStream_t st, c
 #undef RT_CASE
 }
 
-template <bool TRANSP>
+template <bool TRANSP, bool TREE = false>
 hipError_t launch_trace_rays(int depth, dim3 grid, hipStream_t st, const DevScene* s, const double* a,
                              const double* b, int n, double* rgb, uint32_t* rc) {
 #define RT_CASE(k)                                                                                      \
     case k:                                                                                             \
-        hipLaunchKernelGGL((rt_trace_rays_kernel<k, TRANSP>), grid, dim3(kThreads), slot_bytes(k, TRANSP), st, s, \
+        hipLaunchKernelGGL((rt_trace_rays_kernel<k, TRANSP, TREE>), grid, dim3(kThreads), TREE ? 0 : slot_bytes(k, TRANSP), st, s, \
                            a, b, n, rgb, rc);                                                           \
         break;
     switch (depth) {
@@ -536,6 +544,7 @@ struct rt_ctx {
     int n_lights = 0;
     bool scene_set = false;
     bool transparent = false;                  // some material is transparent: TRANSP kernel variants
+    bool tree = false;                         // some material transmits and reflects: TREE kernel variants
     bool eye_valid = false;                    // the device *Prim arrays hold data for `eye`
     bool ever_captured = false;                // a render was captured into a hipGraph: replays may rewrite
                                                // the per-eye data, so every later render re-prepares it
@@ -669,6 +678,7 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     c->n_padded = h->n_padded;
     c->n_lights = h->n_lights;
     c->transparent = h->transparent != 0 || h->n_meshes > 0;   // FULL kernel variants
+    c->tree = h->tree != 0;
     c->eye_valid = false;
     c->scene_set = true;
     c->blob.swap(blob);
@@ -798,7 +808,9 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     const bool cull = c->n_padded >= kConeMin, mw5 = c->min_waves >= 5 && depth <= 3;
     float4* o32 = reinterpret_cast<float4*>(rgba32f);
     uchar4* o8 = reinterpret_cast<uchar4*>(rgba8);
-    if (c->transparent)
+    if (c->tree)
+        e = launch_render_lds<0, 1, true, false, 64, true>(depth, grid, 0, st, c->d_scene, P, o32, o8, rgb64f, raycount);
+    else if (c->transparent)
         e = launch_render_lds<0, 1, true, false, 64>(depth, grid, lds64, st, c->d_scene, P, o32, o8, rgb64f, raycount);
     else if (c->use_lds)
         e = launch_render_lds<1, 1, false, false, kThreads>(depth, grid, c->lds_bytes + lds256, st, c->d_scene, P,
@@ -895,7 +907,8 @@ extern "C" int rt_trace_rays_dev(rt_ctx* c, const double* starts, const double* 
     if (n == 0) return RT_OK;
     RT_HIP(hipSetDevice(c->device));
     dim3 grid((unsigned)((n + kThreads - 1) / kThreads));
-    hipError_t e = (c->transparent ? launch_trace_rays<true> : launch_trace_rays<false>)(
+    hipError_t e = (c->tree ? launch_trace_rays<true, true>
+                    : c->transparent ? launch_trace_rays<true> : launch_trace_rays<false>)(
         depth, grid, (hipStream_t)stream, c->d_scene, starts, ends, n, rgb64f, raycount);
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_trace_rays_kernel: ") + hipGetErrorString(e));
     return RT_OK;

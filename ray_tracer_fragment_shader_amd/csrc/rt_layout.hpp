@@ -45,9 +45,13 @@ struct alignas(16) DevTri {            // Triangle after its ctor (:406-433), ve
 struct alignas(16) DevMat {            // the colour terms rayTraceRay reads (:1224-1226) and its continuation
     double amb[3], diff[3], spec[3];
     double w[3];                       // weight of the child colour: transparency (transmit) or 1 - T (reflect)
+    double wt[3];                      // ray trees: weight of the transmitted child, T (:1241)
+    double wo[3];                      // ray trees: weight of the reflected child, 1 - T (:1246)
     double refr;                       // refraction ratio (transmitted ray, :686-697)
     int32_t transmit;                  // 1: transmitted ray (:1238-1242), 0: reflected ray (:1243-1247)
     int32_t transparent;               // transparency != 0: a shadow blocker of this material lets light pass (:1221)
+    int32_t reflect;                   // opacity != 0: a reflected ray (:1243); with transmit: both (a ray tree)
+    int32_t pad;
 };
 
 struct alignas(16) DevMesh {           // Tetrahedron / Cube Shape (:863-950)
@@ -114,7 +118,7 @@ struct alignas(16) DevScene {
     int32_t n_meshes;
     int32_t n_tris;
     int32_t transparent;               // some material is transparent: closest-hit shadows, weighted children
-    int32_t pad0;
+    int32_t tree;                      // some material transmits AND reflects: ray-tree kernels (trace_tree)
     DevTri tri[2];                     // board triangles T1 = (P1,P2,P3), T2 = (P1,P3,P4)   (:840-841)
     DevMat mat[5];                     // 0 white square, 1 black square, 2 sphere, 3 tetrahedron, 4 cube
     DevLight light[16];

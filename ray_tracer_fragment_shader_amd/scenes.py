@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import ctypes
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 from . import abi
 
@@ -75,6 +75,9 @@ class Scene:
     lights: List[LightSpec] = field(default_factory=list)
     has_board: bool = True
     meshes: List[MeshSpec] = field(default_factory=list)
+    # material overrides: index (MATERIALS order) -> (ambient, diffuse, specular, transparency, refraction);
+    # the others keep the reference's globals (MySdlApplication.cpp:583-588)
+    materials: Optional[Dict[int, tuple]] = None
     _keep: list = field(default_factory=list, repr=False)
 
     def to_abi(self) -> abi.rt_scene:
@@ -98,6 +101,11 @@ class Scene:
             msh[k].after_spheres = m.after_spheres
             msh[k].position = abi.vec3(convert_string_coordinate(m.square))
             msh[k].edge = float(m.edge)
+        for k, m in (self.materials or {}).items():
+            mat = getattr(s, MATERIALS[k])
+            amb, dif, spe, tra, refr = m
+            mat.ambient, mat.diffuse, mat.specular = abi.vec3(amb), abi.vec3(dif), abi.vec3(spe)
+            mat.transparency, mat.refraction = abi.vec3(tra), float(refr)
         s.n_spheres, s.n_lights, s.n_meshes = ns, nl, nm
         s.spheres = ctypes.cast(sph, ctypes.POINTER(abi.rt_sphere))
         s.lights = ctypes.cast(lts, ctypes.POINTER(abi.rt_light))
@@ -115,6 +123,16 @@ class Scene:
             if k < len(self.spheres):
                 out.append(("S", k))
         out.extend(("M", i) for i in range(m, len(self.meshes)))
+        return out
+
+    def material_values(self) -> List[float]:
+        """The five materials as 5 x 13 doubles (ambient, diffuse, specular, transparency, refraction), the
+        layout of oracle/ref_harness.cpp's ref_set_materials."""
+        s = self.to_abi()
+        out: List[float] = []
+        for name in MATERIALS:
+            m = getattr(s, name)
+            out += list(m.ambient) + list(m.diffuse) + list(m.specular) + list(m.transparency) + [m.refraction]
         return out
 
     # the reference harness (oracle/_ref) rebuilds the same scene from the reference's own classes
@@ -138,6 +156,11 @@ class Scene:
         lsq = "".join(lt.square for lt in self.lights).encode()
         lcol = (ctypes.c_double * max(3 * nl, 1))(*[c for lt in self.lights for c in lt.color])
         return (children, len(toks), yoff, rad, edges, lsq, lcol, nl)
+
+
+# rt_scene material fields in the reference's global order (g_whiteSquare, g_blackSquare, g_sphereMaterial,
+# g_tetrahedronMaterial, g_cubeMaterial: MySdlApplication.cpp:583-588)
+MATERIALS = ("white_square", "black_square", "sphere_material", "tetrahedron_material", "cube_material")
 
 
 def load_scene(entries: Sequence[Tuple[str, int]]) -> Scene:
@@ -224,6 +247,29 @@ CONFIGS = {
     # the reference app's own demo frame: initScene's objects, 500x500 window, unit pitch, MAX_DEPTH 5
     "demo": Config("demo", 500, 500, 1, 1, 5),
 }
+
+# Ray-tree scenes (tests only): a material that both transmits and reflects makes rayTraceRay recurse into
+# two children per hit (MySdlApplication.cpp:1238-1247).  The app's own materials never do; these override
+# the reference's material globals (the reference build's harness sets the same values: ref_set_materials).
+GLASS = ((0.0, 0.0, 0.0), (0.1, 0.1, 0.1), (1.0, 1.0, 1.0), (0.4, 0.3, 0.2), 1.3)
+TREE_CASES = {
+    # name: (base config, material overrides, depth, full-size frame for the fixtures' hash)
+    "tree_c2": ("c2", {2: GLASS}, 3, (1920, 1080)),
+    "tree_demo": ("demo", {3: ((0.0, 0.0, 0.0), (0.0, 0.0, 0.0), (0.1, 0.1, 0.1), (0.5, 0.5, 0.5), 2.0 / 3.0)}, 5,
+                  (500, 500)),
+    "tree_c3": ("c3", {0: ((0.1, 0.1, 0.1), (0.5, 0.5, 0.5), (1.0, 1.0, 1.0), (0.25, 0.25, 0.25), 1.0),
+                       2: ((0.0, 0.0, 0.0), (0.1, 0.1, 0.1), (1.0, 1.0, 1.0), (0.6, 0.6, 0.6), 1.5)}, 4, (1280, 720)),
+}
+
+
+def tree_case(name: str):
+    """-> (scene, config, depth, (W, H)) of a TREE_CASES entry."""
+    base, mats, depth, wh = TREE_CASES[name]
+    cfg = CONFIGS[base]
+    sc = cfg.scene()
+    sc.materials = dict(mats)
+    return sc, cfg, depth, wh
+
 
 # Pinned actual-traced ray counts (SURVEY.md §8d, from the reference's rayTraceRay)
 PINNED_RAYS = {"c1": 380_817, "c2": 3_684_271, "c3": 18_956_255, "c5": 90_722_787,

@@ -12,6 +12,9 @@ Outputs (all small, committed):
   kat_<scene>.npz    primitive known-answer tests: rays -> Shape::intersection (hit, material, point,
                      normal, reflected and transmitted ends) and rayTraceRay colours at depth 0..5
   manifest.json      FNV-1a 64 of every full-resolution float64 frame, image sizes, provenance
+  tree_<scene>.npz   ray-tree scenes (scenes.TREE_CASES: partially transparent materials set into the
+                     reference's material globals): small frame, sampled pixels, KAT colours; `--tree`
+                     regenerates only these
 
 Run in the build container (needs /root/reference):  python tests/golden/make_golden.py
 """
@@ -156,9 +159,56 @@ def main() -> None:
                             normal=inter["normal"], reflected_end=inter["reflected_end"],
                             transmitted_end=inter["transmitted_end"], colors=colors)
         print(f"kat_{name}: {len(starts)} rays, {int(inter['hit'].sum())} hits", flush=True)
+    make_tree(manifest)
     with open(os.path.join(OUT, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
 
 
+def canonical_nan(a: np.ndarray) -> np.ndarray:
+    """NaN payloads are not part of the parity contract (the reference's own NaNs come from Line(p, p) on
+    total internal reflection): every NaN becomes the default quiet NaN before hashing."""
+    a = np.array(a, np.float64, copy=True)
+    a[np.isnan(a)] = np.nan
+    return a
+
+
+def make_tree(manifest) -> None:
+    """Ray-tree fixtures (scenes.TREE_CASES): materials that transmit AND reflect, set into the reference's
+    own material globals (oracle/ref_harness.cpp ref_set_materials).  tree_<name>.npz: 160x120 frame,
+    4096 sampled pixels of the full-size frame, KAT rays' rayTraceRay colours at depth 0..depth; the
+    manifest holds the FNV-1a of the full-size frame with NaNs made canonical."""
+    rng = np.random.default_rng(20261016)
+    manifest.setdefault("tree", {})
+    for name in scenes.TREE_CASES:
+        sc, cfg, depth, (W, H) = scenes.tree_case(name)
+        t0 = time.time()
+        small = po.ref_render(sc, SMALL_W, SMALL_H, depth, 500.0 / SMALL_W)
+        pi = rng.integers(0, W, N_SAMPLES).astype(np.int32)
+        pj = rng.integers(0, H, N_SAMPLES).astype(np.int32)
+        samp = po.ref_render_pixels(sc, W, H, depth, 500.0 / W, pi, pj)
+        full = po.ref_render(sc, W, H, depth, 500.0 / W)
+        h = po.fnv1a64(canonical_nan(full))
+        starts, ends, tags = kat_rays(sc, rng)
+        colors = np.stack([po.ref_trace_rays(sc, starts, ends, d) for d in range(depth + 1)])
+        np.savez_compressed(os.path.join(OUT, f"tree_{name[5:]}.npz"), small=small, pi=pi, pj=pj, samples=samp,
+                            small_wh=np.array([SMALL_W, SMALL_H]), depth=np.array(depth), starts=starts, ends=ends,
+                            tags=tags, colors=colors, wh=np.array([W, H]))
+        manifest["tree"][name] = {"width": W, "height": H, "depth": depth, "fnv1a64_canonical_nan": f"{h:016x}",
+                                  "nan_pixels": int(np.isnan(full).any(axis=2).sum()),
+                                  "materials": {str(k): [list(v) if isinstance(v, tuple) else v for v in m]
+                                                for k, m in scenes.TREE_CASES[name][1].items()}}
+        del full
+        print(f"{name}: {time.time() - t0:.1f}s hash {h:016x}", flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--tree"]:                  # only the ray-tree fixtures (the others unchanged)
+        po.build(ref=True)
+        path = os.path.join(OUT, "manifest.json")
+        with open(path) as f:
+            man = json.load(f)
+        make_tree(man)
+        with open(path, "w") as f:
+            json.dump(man, f, indent=1, sort_keys=True)
+    else:
+        main()

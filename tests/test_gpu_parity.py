@@ -227,9 +227,6 @@ def test_errors_are_loud(tr):
     cfg = scenes.CONFIGS["c1"]
     sc = cfg.scene()
     s = sc.to_abi()
-    s.sphere_material.transparency[0] = 0.5          # transmit AND reflect: a ray tree
-    assert L.rt_set_scene(tr._ctx, ctypes.byref(s)) == abi.RT_EUNSUPPORTED
-    s = sc.to_abi()
     s.n_spheres = abi.RT_MAX_SPHERES + 1
     assert L.rt_set_scene(tr._ctx, ctypes.byref(s)) == abi.RT_EINVAL
     tr.set_scene(sc)
@@ -578,3 +575,82 @@ def test_tall_frame_grid_slices(tr):
     want, want_rc = po.render(sc.to_abi(), cam, W, H, 1)
     _assert_parity(rgb, want)
     assert np.array_equal(rc, want_rc)
+
+
+# ---------------------------------------------------------------------------------------------- ray trees
+# Materials that transmit AND reflect (scenes.TREE_CASES): the trace_tree kernels (per-lane node stack)
+# against the reference-generated fixtures and the oracle; NaN positions must agree, payloads are free.
+TREES = list(scenes.TREE_CASES)
+
+
+@pytest.mark.parametrize("name", TREES)
+def test_tree_small_frame_vs_reference(tr, name):
+    sc, cfg, depth, _ = scenes.tree_case(name)
+    g = golden.tree(name)
+    W, H = (int(x) for x in g["small_wh"])
+    rgb, _ = _render64(tr, sc, cfg.camera(W, H), W, H, depth)
+    _assert_parity(rgb, g["small"])
+
+
+@pytest.mark.parametrize("name", TREES)
+def test_tree_samples_and_kat_vs_reference(tr, name):
+    sc, cfg, depth, (W, H) = scenes.tree_case(name)
+    g = golden.tree(name)
+    tr.set_scene(sc)
+    sp = po.screen_points(scenes.make_camera(W, H, 500.0 / W), W, H)[g["pj"], g["pi"]]
+    starts = torch.tensor(np.tile(CAM, (len(sp), 1)), device="cuda")
+    rgb, _ = tr.trace_rays(starts, torch.tensor(np.ascontiguousarray(sp), device="cuda"), depth)
+    _assert_parity(rgb.cpu().numpy(), g["samples"])
+    s = torch.tensor(g["starts"], device="cuda")
+    e = torch.tensor(g["ends"], device="cuda")
+    for d in range(depth + 1):
+        rgb, rc = tr.trace_rays(s, e, d)
+        _assert_parity(rgb.cpu().numpy(), g["colors"][d])
+        _, want_rc = po.trace_rays(sc.to_abi(), g["starts"], g["ends"], d)
+        assert np.array_equal(rc.cpu().numpy().view(np.uint32), want_rc), d
+
+
+@pytest.mark.parametrize("name", TREES)
+def test_tree_full_frame_vs_reference_hash(tr, name):
+    """Full-size tree frame: FNV-1a (NaNs canonical) equals the reference's; ray counts equal the oracle's
+    per pixel; RGBA32F / RGBA8 agree with the FP64 frame."""
+    sc, cfg, depth, (W, H) = scenes.tree_case(name)
+    cam = scenes.make_camera(W, H, 500.0 / W)
+    tr.set_scene(sc)
+    b = tr.render(cam, W, H, depth, rgba32f=True, rgba8=True, rgb64f=True, raycount=True)
+    torch.cuda.synchronize()
+    rgb = b["rgb64f"].cpu().numpy()
+    man = golden.manifest()["tree"][name]
+    assert f"{po.fnv1a64(golden.canonical_nan(rgb)):016x}" == man["fnv1a64_canonical_nan"]
+    _, want_rc = po.render(sc.to_abi(), cam, W, H, depth)
+    assert np.array_equal(b["raycount"].cpu().numpy().view(np.uint32), want_rc)
+    f32 = b["rgba32f"].cpu().numpy()
+    assert np.array_equal(f32[..., :3], rgb.astype(np.float32), equal_nan=True)
+    want8 = np.floor(np.clip(np.nan_to_num(rgb, nan=0.0), 0, 1) * 255.0 + 0.5).astype(np.uint8)
+    assert np.array_equal(b["rgba8"].cpu().numpy()[..., :3], want8)
+
+
+def test_tree_depth_range_and_graph(tr):
+    """Ray trees at every depth 0..7 (the node stack's full size) vs the oracle on a 64 x 48 frame, and a
+    captured tree render replays bit-exact."""
+    sc, cfg, _, _ = scenes.tree_case("tree_c2")
+    W, H = 64, 48
+    cam = cfg.camera(W, H)
+    for depth in range(8):
+        rgb, rc = _render64(tr, sc, cam, W, H, depth)
+        want, want_rc = po.render(sc.to_abi(), cam, W, H, depth)
+        _assert_parity(rgb, want)
+        assert np.array_equal(rc, want_rc), depth
+    tr.set_scene(sc)
+    bufs = tr.alloc(W, H, rgb64f=True)
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        tr.render_into(cam, W, H, 7, bufs, stream=s)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=s):
+        tr.render_into(cam, W, H, 7, bufs, stream=s)
+    bufs["rgb64f"].zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    _assert_parity(bufs["rgb64f"].cpu().numpy(), want)

@@ -157,3 +157,42 @@ def test_screen_faithful_vs_reference_build(name, W, H, seed):
     sc = scenes.CONFIGS[name].scene()
     _, _, calls = po.render_screen(sc.to_abi(), W, H, 5, po.GLIBC, seed)
     assert calls == po.ref_screen_rand_calls(sc, W, H, seed=seed)
+
+
+# ---------------------------------------------------------------------------------------------- ray trees
+# Materials that transmit AND reflect (scenes.TREE_CASES): rayTraceRay's two-child recursion (MSA:1238-1247),
+# pinned to the reference build with the same materials set into its globals.  NaNs (total internal
+# reflection: Line(p, p)) must sit at the same positions; their payloads are not compared.
+TREES = list(scenes.TREE_CASES)
+
+
+@pytest.mark.parametrize("name", TREES)
+def test_tree_small_frame_and_samples(name):
+    sc, cfg, depth, (W, H) = scenes.tree_case(name)
+    g = golden.tree(name)
+    w, h = (int(x) for x in g["small_wh"])
+    rgb, _ = po.render(sc.to_abi(), cfg.camera(w, h), w, h, depth)
+    assert np.array_equal(rgb, g["small"], equal_nan=True)
+    sp = po.screen_points(scenes.make_camera(W, H, 500.0 / W), W, H)[g["pj"], g["pi"]]
+    starts = np.tile(np.array([0.0, 100.0, 200.0]), (len(sp), 1))
+    got, _ = po.trace_rays(sc.to_abi(), starts, sp, depth)
+    assert np.array_equal(got, g["samples"], equal_nan=True)
+
+
+@pytest.mark.parametrize("name", TREES)
+def test_tree_kat_colors(name):
+    sc, cfg, depth, _ = scenes.tree_case(name)
+    g = golden.tree(name)
+    for d in range(depth + 1):
+        got, _ = po.trace_rays(sc.to_abi(), g["starts"], g["ends"], d)
+        assert np.array_equal(got, g["colors"][d], equal_nan=True), d
+
+
+@pytest.mark.parametrize("name", TREES)
+def test_tree_full_frame_hash(name):
+    sc, cfg, depth, (W, H) = scenes.tree_case(name)
+    rgb, rc = po.render(sc.to_abi(), scenes.make_camera(W, H, 500.0 / W), W, H, depth)
+    man = golden.manifest()["tree"][name]
+    assert f"{po.fnv1a64(golden.canonical_nan(rgb)):016x}" == man["fnv1a64_canonical_nan"]
+    assert int(np.isnan(rgb).any(axis=2).sum()) == man["nan_pixels"]
+    assert (rc & 0xFFFF).max() > depth + 1          # some pixel branched (more segments than a chain)
