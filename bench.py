@@ -62,7 +62,7 @@ def parse():
                     help="skip parity/ray-count/cpu and extra legs (for rocprofv3 runs)")
     ap.add_argument("--no-c4", action="store_true", help="skip the c4 (row split + RCCL gather) leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the c3/c5 and drop-in legs (N = 1)")
-    ap.add_argument("--frames-in-flight", type=int, default=2,
+    ap.add_argument("--frames-in-flight", type=int, default=3,
                     help="independent frames round-robin over this many HIP streams, each with its own context and "
                          "output buffers, so a frame's launch starts while the previous frame's last waves drain "
                          "(1: one stream, launches back to back)")
