@@ -265,6 +265,7 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
 // index), so the longest rows are dispatched first and the cheap ones fill the tail (longest-processing-
 // time-first list scheduling).  One workgroup, bitonic sort of (~cost, row) keys in LDS; n <= kOrderMax.
 constexpr int kOrderMax = 8192;
+constexpr int kRecalibrate = 8;                // renders of a moving camera per re-timing of the tile rows
 __global__ __launch_bounds__(1024) void rt_order_kernel(const uint32_t* __restrict__ cost, int n,
                                                         int32_t* __restrict__ order) {
     __shared__ uint64_t key[kOrderMax];
@@ -556,9 +557,12 @@ struct rt_ctx {
     int wg_staging = 0;                        // RT_WG_STAGING=1: LDS-staged 32-pixel row stores (A/B)
     // Adaptive tile-row order (rt_order_kernel): the first render of a new (scene, camera, size, rows,
     // depth, outputs) view uses the identity order; the second render of the same view is a calibration
-    // render that also times its tile rows; later renders dispatch the rows by decreasing time (a camera
-    // that moves every frame never pays for a calibration).  order_mode (rt_diag_tile_order): 0 adaptive,
-    // 1 bottom-to-top.
+    // render that also times its tile rows; later renders dispatch the rows by decreasing time.  A render
+    // of another camera with the same frame shape (size, rows, depth, outputs, scene) reuses the last
+    // calibrated order — row costs change slowly with the camera — and every kRecalibrate-th such render
+    // re-times the rows under it, so a moving camera keeps a longest-first order without paying for a
+    // calibration every frame.  Any order is a permutation of the tile rows: images never depend on it.
+    // order_mode (rt_diag_tile_order): 0 adaptive, 1 bottom-to-top.
     int32_t* d_tile_rows = nullptr;
     uint32_t* d_row_cost = nullptr;
     int n_tile_rows = 0;                       // capacity of both (kOrderMax, allocated by rt_ctx_create)
@@ -567,6 +571,7 @@ struct rt_ctx {
     ViewKey order_key{};
     bool seen_valid = false;                   // `seen_key`: the last view rendered once in identity order
     ViewKey seen_key{};
+    int stale = 0;                             // renders of other cameras since the order was calibrated
     int order_mode = 0;
     uint64_t scene_gen = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -777,8 +782,19 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
         if (rows) memcpy(kp, rows, sizeof(rt_rows));
         kp += sizeof(rt_rows);
         memcpy(kp, &c->scene_gen, sizeof(uint64_t));
+        constexpr size_t kCam = sizeof(rt_camera);
+        const bool same_shape = c->order_valid &&
+                                memcmp(key.data() + kCam, c->order_key.data() + kCam, key.size() - kCam) == 0;
         if (c->order_valid && key == c->order_key) {
             P.tile_rows = c->d_tile_rows;
+        } else if (same_shape) {
+            P.tile_rows = c->d_tile_rows;               // another camera: the last calibrated order
+            if (++c->stale >= kRecalibrate) {           // ... re-timed every kRecalibrate-th render
+                RT_HIP(hipMemsetAsync(c->d_row_cost, 0, sizeof(uint32_t) * tiles_y, st));
+                P.row_cost = c->d_row_cost;
+                calibrate = true;
+                c->order_valid = false;
+            }
         } else if (c->seen_valid && key == c->seen_key) {
             RT_HIP(hipMemsetAsync(c->d_row_cost, 0, sizeof(uint32_t) * tiles_y, st));
             P.row_cost = c->d_row_cost;                 // calibration render (identity order)
@@ -833,6 +849,7 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
         if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_order_kernel: ") + hipGetErrorString(e));
         c->order_key = key;                             // only once the order kernel is queued
         c->order_valid = true;
+        c->stale = 0;
     }
     return RT_OK;
 }

@@ -13,7 +13,7 @@ while read -r group; do
   [ -z "$group" ] && continue
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $group --kernel-trace --output-format csv -d "$OUT/p$i" -o run -- \
-     python3 "$ROOT/bench.py" --config ${CONFIG:-c2} --steps 10 --warmup 2 --profile-kernel-only \
+     python3 "$ROOT/bench.py" --config ${CONFIG:-c2} --steps 10 --warmup 2 --profile-kernel-only --frames-in-flight 1 \
      > "$OUT/p$i.log" 2>&1 || { echo "pass $i ($group) failed rc=$?"; tail -5 "$OUT/p$i.log"; exit 5; }
   echo "pass $i ok: $group"
 done < <(if [ -n "${PMC_GROUPS:-}" ]; then echo "$PMC_GROUPS" | tr ';' '\n'; else cat <<'GROUPS'
