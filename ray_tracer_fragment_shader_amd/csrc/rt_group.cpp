@@ -9,9 +9,11 @@
 //
 //   render stream rs_r:  wait sent[r][b] -> rt_render_dev(rows of r) into slab[r][b] -> record rendered[r][b]
 //   comm stream   cs_r:  wait rendered[r][b] -> ncclSend(slab[r][b] -> rank 0)      -> record sent[r][b]
-//   root cs_0:           wait assembled[b]   -> ncclRecv(gathered[b] + q*slab <- q), q = 0..n-1 (q = 0: self)
-//                        -> record received[b]
-//   caller stream (root): wait received[b] -> rt_unshuffle_dev(gathered[b] -> image) -> record assembled[b]
+//   root cs_0:           wait rendered[b] -> ncclRecv(gathered[b] + q*slab <- q), q = 1..n-1; wait the caller
+//                        stream's earlier work (received[b]) -> unshuffle(gathered[b] + root slab[b] -> image)
+//                        -> record assembled[b]; the caller's stream waits for assembled[b]
+// Stream priorities: rs lowest, cs highest (the gather's kernels do not queue behind the next render grid).
+// A one-rank group renders straight into the caller's image on the caller's stream (identity band plan).
 //
 // b = frame & 1: the slabs and the root's gather buffer are double-buffered, so frame f's gather overlaps
 // frame f+1's render.  Transports: RCCL (ncclCommInitAll for one process driving n GPUs, ncclCommInitRank
@@ -93,8 +95,13 @@ int setup_rank(Rank* r, rt_ctx* ctx, int rank, hipEvent_t* sent_device_events) {
     r->rank = rank;
     r->device = rt_ctx_device(ctx);
     G_HIP(hipSetDevice(r->device));
-    G_HIP(hipStreamCreateWithFlags(&r->rs, hipStreamNonBlocking));
-    G_HIP(hipStreamCreateWithFlags(&r->cs, hipStreamNonBlocking));
+    // The render stream gets the lowest priority and the comm stream (RCCL send/recv, and on the root the
+    // unshuffle) the highest: a frame's gather kernels are dispatched as soon as CUs free up instead of
+    // queueing behind the next frame's render grid, so the exchange overlaps the render.
+    int least = 0, greatest = 0;
+    G_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    G_HIP(hipStreamCreateWithPriority(&r->rs, hipStreamNonBlocking, least));
+    G_HIP(hipStreamCreateWithPriority(&r->cs, hipStreamNonBlocking, greatest));
     for (int b = 0; b < 2; ++b) {
         G_HIP(hipEventCreateWithFlags(&r->rendered[b], hipEventDisableTiming));
         if (!sent_device_events) G_HIP(hipEventCreateWithFlags(&r->sent[b], hipEventDisableTiming));
@@ -277,6 +284,20 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     const int b = (int)(g->frame & 1);
     const hipStream_t st = (hipStream_t)stream;
 
+    // ---- one rank: the band plan is the identity, so the frame is rendered straight into the caller's image
+    // on the caller's stream (no slab, no unshuffle, no cross-stream hand-off: each one costs ~30 us) ----
+    if (g->n_ranks == 1) {
+        Rank& r = g->ranks[0];
+        G_HIP(hipSetDevice(r.device));
+        rc = rt_render_dev(r.ctx, cam, W, H, depth, nullptr, kind_on[0] ? rgba32f : nullptr,
+                           kind_on[1] ? rgba8 : nullptr, nullptr, nullptr, st);
+        if (rc) return rc;
+        g->last_band = hb;
+        g->last_slab_rows = slab_rows;
+        ++g->frame;
+        return RT_OK;
+    }
+
     // ---- buffers (grow-only; a size change waits for the frames still using them) -----------------------
     const bool regrow = hb != g->last_band || slab_rows != g->last_slab_rows;
     if (regrow && g->frame > 0) {
@@ -307,6 +328,8 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     for (auto& r : g->ranks) {
         G_HIP(hipSetDevice(r.device));
         if (r.sent_rec[b]) G_HIP(hipStreamWaitEvent(r.rs, r.sent[b], 0));     // slab[b] has left (frame - 2)
+        if (r.rank == 0 && g->assembled_rec[b])                               // the root's slab[b] is read by
+            G_HIP(hipStreamWaitEvent(r.rs, g->assembled[b], 0));              // frame - 2's unshuffle
         rt_rows rows = {hb, g->n_ranks, r.rank, 1};
         rc = rt_render_dev(r.ctx, cam, W, H, depth, &rows, (float*)r.slab[b][0], (uint8_t*)r.slab[b][1], nullptr,
                            nullptr, r.rs);
@@ -337,13 +360,14 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
             for (int k = 0; k < kKinds; ++k) {
                 if (!kind_on[k]) continue;
                 const size_t bytes = (size_t)rows_of(r.rank) * W * kElem[k];
-                ncclResult_t e = ncclSend(r.slab[b][k], bytes, ncclUint8, 0, r.comm, r.cs);
+                ncclResult_t e = ncclSuccess;
+                if (r.rank != 0) e = ncclSend(r.slab[b][k], bytes, ncclUint8, 0, r.comm, r.cs);
                 if (e != ncclSuccess) {
                     (void)ncclGroupEnd();
                     return rt_fail(RT_EHIP, std::string("ncclSend: ") + ncclGetErrorString(e));
                 }
                 if (r.rank != 0) continue;
-                for (int q = 0; q < g->n_ranks; ++q) {
+                for (int q = 1; q < g->n_ranks; ++q) {        // the root's own slab is unshuffled in place
                     char* dst = (char*)g->gathered[b][k] + (size_t)q * slab_rows * W * kElem[k];
                     e = ncclRecv(dst, (size_t)rows_of(q) * W * kElem[k], ncclUint8, q, r.comm, r.cs);
                     if (e != ncclSuccess) {
@@ -365,7 +389,7 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         for (auto& r : g->ranks) {
             G_HIP(hipStreamWaitEvent(root.cs, r.rendered[b], 0));
             for (int k = 0; k < kKinds; ++k) {
-                if (!kind_on[k]) continue;
+                if (!kind_on[k] || r.rank == 0) continue;      // the root's own slab is unshuffled in place
                 char* dst = (char*)g->gathered[b][k] + (size_t)r.rank * slab_rows * W * kElem[k];
                 G_HIP(hipMemcpyPeerAsync(dst, root.device, r.slab[b][k], r.device,
                                          (size_t)rows_of(r.rank) * W * kElem[k], root.cs));
@@ -375,18 +399,23 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         }
     }
 
-    // ---- assemble on rank 0, ordered on the caller's stream --------------------------------------------------
+    // ---- assemble on rank 0 (high-priority comm stream), ordered before the caller's stream's later work ----
+    // The caller's image is written by this frame's unshuffle: its stream waits for `received` (the previous
+    // frame's image may still be read there) before the unshuffle is queued behind it on the comm stream.
     if (g->owns_root) {
         Rank& root = g->ranks[0];
         G_HIP(hipSetDevice(root.device));
-        G_HIP(hipEventRecord(g->received[b], root.cs));
-        G_HIP(hipStreamWaitEvent(st, g->received[b], 0));
+        G_HIP(hipEventRecord(g->received[b], st));                   // caller's earlier work on the image
+        G_HIP(hipStreamWaitEvent(root.cs, g->received[b], 0));
         for (int k = 0; k < kKinds; ++k) {
             if (!kind_on[k]) continue;
-            rc = rt_unshuffle_dev(g->gathered[b][k], outs[k], W, H, (int)kElem[k], hb, g->n_ranks, slab_rows, st);
+            rc = rt_unshuffle_dev_ex(g->gathered[b][k], root.slab[b][k], outs[k], W, H, (int)kElem[k], hb, g->n_ranks,
+                                     slab_rows, root.cs);
             if (rc) return rc;
         }
-        G_HIP(hipEventRecord(g->assembled[b], st));
+        G_HIP(hipSetDevice(root.device));
+        G_HIP(hipEventRecord(g->assembled[b], root.cs));
+        G_HIP(hipStreamWaitEvent(st, g->assembled[b], 0));
         g->assembled_rec[b] = true;
     }
     ++g->frame;

@@ -19,3 +19,8 @@ void rt_camera_basis(const rt_camera* cam, double right[3], double upp[3]);
 
 // Device ordinal of a context (rt_group.cpp).
 int rt_ctx_device(const rt_ctx* ctx);
+
+// rt_unshuffle_dev with rank 0's rows read from `rank0_slab` instead of the gathered buffer (the group's root
+// unshuffles its own slab in place of sending it to itself); rank0_slab = nullptr: from `gathered`.
+int rt_unshuffle_dev_ex(const void* gathered, const void* rank0_slab, void* image, int W, int H, int elem_bytes,
+                        int band_height, int n_ranks, int slab_rows, void* stream);

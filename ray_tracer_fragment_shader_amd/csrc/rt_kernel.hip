@@ -417,8 +417,12 @@ __global__ __launch_bounds__(kThreads) void rt_intersect_kernel(const DevScene* 
     hits[k] = h;
 }
 
-// One workgroup per image row; copies the row from its rank's slab, 4 bytes per work-item step.
+// One workgroup per image row; copies the row from its rank's slab (rank 0's from src0 when given: the
+// group's root does not send its own slab to itself), 16 bytes per work-item step when rows are 16-byte
+// multiples (RGBA8 rows of W % 4 == 0, every RGBA32F row), else 4.
+template <int VEC>
 __global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* __restrict__ src,
+                                                                const uint32_t* __restrict__ src0,
                                                                 uint32_t* __restrict__ dst, int row_words,
                                                                 int height, int band_height, int n_ranks,
                                                                 int slab_rows) {
@@ -427,9 +431,16 @@ __global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* 
     const int band = j / band_height;
     const int rank = band % n_ranks;
     const int lr = (band / n_ranks) * band_height + (j - band * band_height);
-    const uint32_t* s = src + ((size_t)rank * slab_rows + lr) * row_words;
+    const uint32_t* s = (rank == 0 && src0) ? src0 + (size_t)lr * row_words
+                                            : src + ((size_t)rank * slab_rows + lr) * row_words;
     uint32_t* d = dst + (size_t)j * row_words;
-    for (int w = threadIdx.x; w < row_words; w += kThreads) d[w] = s[w];
+    if (VEC == 4) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(s);
+        uint4* d4 = reinterpret_cast<uint4*>(d);
+        for (int w = threadIdx.x; w < (row_words >> 2); w += kThreads) d4[w] = s4[w];
+    } else {
+        for (int w = threadIdx.x; w < row_words; w += kThreads) d[w] = s[w];
+    }
 }
 
 // rt_render's ray statistics: sums of the per-pixel counters (primary+reflect segments, shadow rays) into
@@ -945,8 +956,8 @@ extern "C" int rt_intersect_dev(rt_ctx* c, const double* starts, const double* e
     return RT_OK;
 }
 
-extern "C" int rt_unshuffle_dev(const void* gathered, void* image, int W, int H, int elem_bytes, int band_height,
-                                int n_ranks, int slab_rows, void* stream) {
+int rt_unshuffle_dev_ex(const void* gathered, const void* rank0_slab, void* image, int W, int H, int elem_bytes,
+                        int band_height, int n_ranks, int slab_rows, void* stream) {
     if (!gathered || !image) return rt_fail(RT_EINVAL, "rt_unshuffle_dev: null buffer");
     if (W <= 0 || H <= 0 || band_height <= 0 || n_ranks <= 0 || slab_rows < 0)
         return rt_fail(RT_EINVAL, "rt_unshuffle_dev: bad geometry");
@@ -960,11 +971,18 @@ extern "C" int rt_unshuffle_dev(const void* gathered, void* image, int W, int H,
         if (nl > slab_rows) return rt_fail(RT_EINVAL, "rt_unshuffle_dev: slab_rows smaller than a rank's rows");
     }
     const int row_words = (int)(((long long)W * elem_bytes) / 4);
-    hipLaunchKernelGGL(rt_unshuffle_kernel, dim3((unsigned)H), dim3(kThreads), 0, (hipStream_t)stream,
-                       (const uint32_t*)gathered, (uint32_t*)image, row_words, H, band_height, n_ranks, slab_rows);
+    const bool vec = row_words % 4 == 0 && ((uintptr_t)gathered | (uintptr_t)rank0_slab | (uintptr_t)image) % 16 == 0;
+    auto k = vec ? rt_unshuffle_kernel<4> : rt_unshuffle_kernel<1>;
+    hipLaunchKernelGGL(k, dim3((unsigned)H), dim3(kThreads), 0, (hipStream_t)stream, (const uint32_t*)gathered,
+                       (const uint32_t*)rank0_slab, (uint32_t*)image, row_words, H, band_height, n_ranks, slab_rows);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_unshuffle_kernel: ") + hipGetErrorString(e));
     return RT_OK;
+}
+
+extern "C" int rt_unshuffle_dev(const void* gathered, void* image, int W, int H, int elem_bytes, int band_height,
+                                int n_ranks, int slab_rows, void* stream) {
+    return rt_unshuffle_dev_ex(gathered, nullptr, image, W, H, elem_bytes, band_height, n_ranks, slab_rows, stream);
 }
 
 // Diagnostics (include/rt_diag.h): tile-row dispatch order of later renders: 0 adaptive (default), 1
