@@ -56,6 +56,18 @@
 #ifndef RT_KEEP_NU
 #define RT_KEEP_NU 0
 #endif
+// 1: rays that start at a board hit skip the board test, rays that start at a sphere hit that sphere's test
+// (certain misses, origin_skip).
+#ifndef RT_BOARD_SKIP
+#define RT_BOARD_SKIP 1
+#endif
+#ifndef RT_SELF_SKIP
+#define RT_SELF_SKIP 1
+#endif
+// 1: the skips also in the fast (non-CULL) bounce loop; 0: only in the CULL variant.
+#ifndef RT_SKIP_FAST
+#define RT_SKIP_FAST 1
+#endif
 
 namespace rt {
 
@@ -326,6 +338,35 @@ __device__ __forceinline__ bool board_hit(const DevScene* S, d3 p0, d3 d, d3* p)
     return false;
 }
 
+// Tests that a ray starting at the hit point q of the previous level certainly misses (exact skips):
+//  * the board, when q is a board hit of a ray from p0.  The board normal is exactly (0, -1, 0) (host-
+//    checked), so num = n . (v0 - q) = -(v0.y - q.y) with q.y = p0.y + m0 d0.y rounded, m0 = num0 / nd0
+//    rounded: |num| <= 2^-50 (3 |p0.y| + 5 |v0.y| + 1) < eps^2 / 2 whenever |p0.y| <= board_skip_y
+//    (host).  board_hit misses unless |nd| >= eps, and then |m| = |num / nd| (1 + 2^-53) < eps: the m < eps
+//    test (:659) misses.
+//  * sphere k, when q is a hit of sphere k.  Any ray from q has dP = C - q, dd = |dP|^2 (computed here with
+//    the same operations) and |uD| <= sqrt(dd) (1 + 2^-50), so disc = fl(fl(uD^2 - dd) + r2) is within
+//    E = 2^-49 (dd + r2) of uD^2 + g, g = r2 - dd.  uD < 0 gives s < 0; otherwise
+//    |s| <= sqrt(|g| + E) + 2^-51 sqrt(dd + r2) < eps when |g| + E < eps^2 / 4 (self_eps2): the near root
+//    misses (:754, :767) — the reference never uses the far root.
+// NaN / inf operands fail the compares (no skip).  Returns -1 (no skip), 0 (board) or 1 + k (sphere k).
+__device__ __forceinline__ int origin_skip(const SceneView& V, int kind, d3 p0, d3 q) {
+    const DevScene* S = V.S;
+    if (RT_BOARD_SKIP && kind == 0) return fabs(p0.y) <= S->board_skip_y ? 0 : -1;
+    if (RT_SELF_SKIP && kind >= 1 && kind < kMeshKind) {
+        const DevSphere& sp = V.sph[kind - 1];
+        const d3 dP = sub(ld3(sp.c), q);
+        const double dd = dot(dP, dP);
+        return fabs(sp.r2 - dd) + 0x1p-49 * (dd + sp.r2) < S->self_eps2 ? kind : -1;
+    }
+    return -1;
+}
+
+// Clears sphere `self` (origin_skip - 1) from the pass bits of the batch starting at k0.
+__device__ __forceinline__ uint32_t drop_self(uint32_t pass, int self, int k0) {
+    return (unsigned)(self - k0) < (unsigned)kChunk ? pass & ~(1u << (self - k0)) : pass;
+}
+
 // Triangle::intersection (:611-707) on a mesh triangle, with the same division-skipping sign tests as
 // board_hit.  d = end - start (unnormalised).
 __device__ __forceinline__ bool tri_hit(const DevTri& T, d3 p0, d3 d, double eps, d3* p) {
@@ -465,10 +506,11 @@ __device__ __forceinline__ uint64_t sphere_bits(int np) { return np >= 64 ? ~0ul
 // in SGPRs), then each lane runs the exact FP64 test only on its own surviving spheres, in increasing k,
 // so the strict-< closest-hit order of the reference is unchanged.  Padding spheres never survive.
 __device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const Ray& r, int k0, double eps,
-                                                     int* kind, double* best, d3* hp) {
+                                                     int* kind, double* best, d3* hp, int self = -1) {
     uint32_t pass = 0;
 #pragma unroll
     for (int j = 0; j < kChunk; ++j) pass |= (sphere_reject32(V.sphf[k0 + j], r) ? 0u : 1u) << j;
+    pass = drop_self(pass, self, k0);                       // r starts on sphere `self`: a certain miss
 #if RT_UNIFORM_SECONDARY
 #pragma unroll
     for (int j = 0; j < kChunk; ++j) {
@@ -493,13 +535,15 @@ __device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const R
 
 // `mask` (np >= kConeMin): spheres k < 64 this wave's rays may hit (ray_bundle_mask); the rest of the
 // first 64 are skipped.  Spheres are visited in increasing k either way.
+// skip = origin_skip of r's origin: 0 skips the board test, 1 + k sphere k's (certain misses).
 template <bool FULL, bool CULL = false>
-__device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3* hp, uint64_t mask = ~0ull) {
+__device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3* hp, uint64_t mask = ~0ull,
+                                           int skip = -1) {
     const DevScene* S = V.S;
     if (!bound_pass(S, r.p0, r.u)) return -1;
     int kind = -1;
     double best = -1.0;
-    if (S->has_board) {
+    if (S->has_board && skip != 0) {
         d3 q;
         if (board_hit(S, r.p0, r.d, &q)) {
             kind = 0;
@@ -512,7 +556,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
     if (CULL && V.np >= kConeMin) {
         for (uint64_t m = mask & sphere_bits(V.np); m; m &= m - 1) {
             const int k = __builtin_ctzll(m);
-            if (sphere_reject32(V.sphf[k], r)) continue;
+            if (k == skip - 1 || sphere_reject32(V.sphf[k], r)) continue;
             d3 q;
             if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) {
                 double dist = len_fast(sub(q, r.p0));       // :811-812
@@ -525,7 +569,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
         }
         k0 = 64;
     }
-    for (; k0 < V.np; k0 += kChunk) sphere_batch_closest(V, r, k0, eps, &kind, &best, hp);
+    for (; k0 < V.np; k0 += kChunk) sphere_batch_closest(V, r, k0, eps, &kind, &best, hp, skip - 1);
     if (FULL) meshes_closest(V, r, eps, &kind, &best, hp);
     return kind;
 }
@@ -767,7 +811,8 @@ __device__ __forceinline__ uint64_t shadow_bundle_mask(const SceneView& V, bool 
 // relative, likewise covered.  A NaN direction is not rejected (it compares false), as the FP64 test
 // reports NaN rays as hits.
 template <bool FULL, bool CULL = false>
-__device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull) {
+__device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull,
+                                         int skip = -1) {
     const DevScene* S = V.S;
     if (!bound_pass(S, r.p0, r.u)) return false;
     const double eps = S->eps;
@@ -780,7 +825,7 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
             float t = r.ux * f.vx;
             t = fmaf(r.uy, f.vy, t);
             t = fmaf(r.uz, f.vz, t);
-            if (fabsf(t) < f.c) continue;
+            if (fabsf(t) < f.c || k == skip - 1) continue;
             d3 q;
             if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) return true;
         }
@@ -796,6 +841,7 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
             t = fmaf(r.uz, f.vz, t);
             pass |= (fabsf(t) < f.c ? 0u : 1u) << j;
         }
+        pass = drop_self(pass, skip - 1, k0);
 #if RT_UNIFORM_SHADOW
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
@@ -810,7 +856,7 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
             if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) return true;
         }
     }
-    if (S->has_board) {
+    if (S->has_board && skip != 0) {
         d3 q;
         if (board_hit(S, r.p0, r.d, &q)) return true;
     }
@@ -887,7 +933,8 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
 // lanes of the wave, the light loop stays converged for shadow_bundle_mask; otherwise only by hit lanes.
 // FULL: meshes may be present and materials may be transparent (closest-hit shadows, :1219-1221).
 template <bool FULL, bool CULL>
-__device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, int mat, double ks) {
+__device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, int mat, double ks,
+                                    int skip = -1) {
     const DevScene* S = V.S;
     d3 color = mk(0.0, 0.0, 0.0);
     Ray sr;
@@ -903,7 +950,7 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
         uint64_t m = ~0ull;
         if (CULL && !FULL && V.np >= kConeMin) m = shadow_bundle_mask(V, hit, sr, i);
         bool lit = false;
-        if (hit) lit = !(FULL ? occluded_transparent(V, sr) : occluded<false, CULL>(V, sr, i, m));
+        if (hit) lit = !(FULL ? occluded_transparent(V, sr) : occluded<false, CULL>(V, sr, i, m, skip));
         if (lit) {
             const DevMat& M = S->mat[mat];                  // material terms loaded only when lit
             double a = S->att / (S->att + dl * dl);         // attenuation (:1181)
@@ -971,7 +1018,7 @@ __device__ __forceinline__ void next_ray(d3 p, d3 nd, d3 nu, Ray* r) {
 template <int B, bool TRANSP, int SS = kSlotStride>
 __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool first, bool alive, d3 bdP, double bdd,
                                            uint64_t cone, Ray* r, int* levels, uint32_t* nseg, uint32_t* nsh,
-                                           double* slot, int* mslot) {
+                                           double* slot, int* mslot, int* skip) {
     uint64_t smask = ~0ull;
     if (!first) {
         set_origin_f32(V.S, r);
@@ -981,9 +1028,11 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     int kind = -1;
     if (alive) {
         ++*nseg;
-        kind = first ? closest_hit_primary<TRANSP>(V, *r, bdP, bdd, cone, &p) : closest_hit<TRANSP, true>(V, *r, &p, smask);
+        kind = first ? closest_hit_primary<TRANSP>(V, *r, bdP, bdd, cone, &p)
+                     : closest_hit<TRANSP, true>(V, *r, &p, smask, TRANSP ? -1 : *skip);
     }
     const bool hit = kind >= 0;
+    *skip = TRANSP ? -1 : origin_skip(V, kind, r->p0, p);      // this hit's rays start at p
     if (!__any(hit)) return false;
     d3 n = mk(0.0, 0.0, 0.0), nd = n;
     int mat = 0;
@@ -995,7 +1044,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
         ks = fabs(dot(r->u, unit(rd)));                     // |u . reflectedRay.direction()|
         nd = continuation<TRANSP>(V, kind, mat, p, n, r->u, rd);
     }
-    const d3 c = shade<TRANSP, true>(V, hit, p, n, mat, ks);
+    const d3 c = shade<TRANSP, true>(V, hit, p, n, mat, ks, *skip);
     if (hit) {
         park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
         *nsh += V.nl;
@@ -1015,13 +1064,15 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
     d3 d = sub(p1, p0);
     set_dir(&r, d, unit(d));
     uint32_t nseg = 0, nsh = 0;
+    int skip = -1;                                          // origin_skip of r's origin
 #pragma unroll
     for (int lvl = 0; lvl <= B; ++lvl) {
         const bool alive = lvl == 0 || levels == lvl;
         if (!__any(alive)) break;                           // the whole wave has missed: early out
         const bool first = PRIMARY && lvl == 0;
         if (CULL) {
-            if (!cull_level<B, TRANSP, SS>(V, lvl, first, alive, bdP, bdd, cone, &r, &levels, &nseg, &nsh, slot, mslot))
+            if (!cull_level<B, TRANSP, SS>(V, lvl, first, alive, bdP, bdd, cone, &r, &levels, &nseg, &nsh, slot, mslot,
+                                           &skip))
                 break;
         } else {
             d3 p = mk(0.0, 0.0, 0.0);
@@ -1032,10 +1083,11 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                     kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p);
                 } else {
                     set_origin_f32(S, &r);
-                    kind = closest_hit<TRANSP>(V, r, &p);
+                    kind = closest_hit<TRANSP>(V, r, &p, ~0ull, TRANSP ? -1 : skip);
                 }
             }
             const bool hit = kind >= 0;
+            skip = (TRANSP || !RT_SKIP_FAST) ? -1 : origin_skip(V, kind, r.p0, p);   // this hit's rays start at p
             d3 nd = mk(0.0, 0.0, 0.0);
 #if RT_KEEP_NU
             d3 nu = nd;
@@ -1051,7 +1103,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
 #if RT_KEEP_NU
                 nu = (TRANSP && V.S->mat[mat].transmit) ? unit(nd) : rdir;
 #endif
-                const d3 c = shade<TRANSP, false>(V, true, p, n, mat, ks);
+                const d3 c = shade<TRANSP, false>(V, true, p, n, mat, ks, skip);
                 park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
                 nsh += V.nl;
                 levels = lvl + 1;

@@ -395,6 +395,17 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
             return rt_fail(RT_EUNSUPPORTED, "rt_set_scene: half-degenerate board");
         }
     }
+    // Board self-test skip (rt_device.hpp board_skip): with the board normal exactly (0, +-1, 0), a ray that
+    // starts at a board hit point q has |n . (v0 - q)| <= 2^-50 (3 |p0.y| + 5 |v0.y| + 1), p0 the origin of
+    // the ray that hit; below eps^2 / 2 its m = num / nd (|nd| >= eps) is below eps: a certain miss.
+    d->board_skip_y = -1.0;
+    d->self_eps2 = 0.25 * s->small_number * s->small_number;
+    if (d->has_board && d->tri[0].n[0] == 0.0 && d->tri[0].n[2] == 0.0 && std::fabs(d->tri[0].n[1]) == 1.0 &&
+        s->small_number > 0) {
+        const double eps2 = s->small_number * s->small_number;
+        const double y = (eps2 / 2 / 0x1p-50 - 5 * std::fabs(d->tri[0].v0[1]) - 1) / 3;
+        if (y > 0 && std::isfinite(y)) d->board_skip_y = y;
+    }
     for (int m = 0; m < 5; ++m) d->mat[m] = dm[m];
     d->transparent = any_transparent ? 1 : 0;
     d->tree = tree ? 1 : 0;

@@ -107,6 +107,9 @@ struct alignas(16) DevScene {
     double half;                       // BOARD_HALF_SIZE
     double square;                     // SQUARE_EDGE_SIZE
     double rsquare;                    // rcp_core(square), computed on the device (rt_scene_init_kernel)
+    double board_skip_y;               // rays starting at a board hit whose ray came from |y| <= this provably
+                                       // miss the board (rt_device.hpp origin_skip); -1: never skipped
+    double self_eps2;                  // eps^2 / 4: sphere self-test skip threshold (origin_skip)
     double board_num;                  // n . (v0 - eye) of the board plane for the camera `eye` (per eye)
     double eye[3];                     // camera the *Prim arrays and board_num were computed for
     int32_t bound_on;                  // g_scene radius > 0

@@ -654,3 +654,34 @@ def test_tree_depth_range_and_graph(tr):
     g.replay()
     torch.cuda.synchronize()
     _assert_parity(bufs["rgb64f"].cpu().numpy(), want)
+
+
+def test_origin_skips_edge_cases(tr):
+    """The exact skips for rays that start at a hit (origin_skip: the board test after a board hit, a sphere's
+    own test after a hit on it) at their thresholds: rays from far above the board (|p0.y| past
+    board_skip_y, so the board is tested again), tiny / huge / distant spheres (the self-test bound fails and
+    the sphere is tested again), grazing and inward rays; every colour and ray count equals the oracle's."""
+    rng = np.random.default_rng(7)
+    sc = scenes.Scene(spheres=[scenes.SphereSpec("d4", 1e-3), scenes.SphereSpec("e5", 20.0, 1e-9),
+                               scenes.SphereSpec("c3", 5e3, -5e3 - 60.0), scenes.SphereSpec("f6", 20.0, 3e6),
+                               scenes.SphereSpec("b2", 0.5, 30.0)],
+                      lights=[scenes.LightSpec("b6", scenes.WHITE), scenes.LightSpec("g3", scenes.GREY)])
+    tr.set_scene(sc)
+    n = 6144
+    heights = np.concatenate([np.full(n // 6, h) for h in (50.0, 1e3, 5e6, 6e6, 1e9, 1e15)])
+    starts = np.stack([rng.uniform(-150, 150, n), heights, rng.uniform(-310, -10, n)], axis=1)
+    ends = np.stack([rng.uniform(-150, 150, n), np.zeros(n), rng.uniform(-310, -10, n)], axis=1)
+    # rays at the spheres' surfaces, from outside and inside
+    cs = np.array([sp.center() for sp in sc.spheres]) + np.array([0.0, 0.0, -160.0])
+    k = rng.integers(0, len(cs), n)
+    dirs = rng.normal(size=(n, 3))
+    starts2 = cs[k] + dirs * rng.uniform(0.5, 3.0, (n, 1)) * np.array([sp.radius for sp in sc.spheres])[k, None]
+    ends2 = cs[k] + rng.normal(size=(n, 3)) * 0.1
+    s = np.concatenate([starts, starts2])
+    e = np.concatenate([ends, ends2])
+    S, E = torch.tensor(s, device="cuda"), torch.tensor(e, device="cuda")
+    for depth in (1, 3):
+        rgb, rc = tr.trace_rays(S, E, depth)
+        want, want_rc = po.trace_rays(sc.to_abi(), s, e, depth)
+        _assert_parity(rgb.cpu().numpy(), want)
+        assert np.array_equal(rc.cpu().numpy().view(np.uint32), want_rc), depth
