@@ -740,14 +740,16 @@ __device__ __forceinline__ uint64_t ray_bundle_mask(const SceneView& V, bool on,
     const int f = __builtin_ctzll(onm);
     const float ox = lane_f32(r.px, f), oy = lane_f32(r.py, f), oz = lane_f32(r.pz, f);
     const float ax = lane_f32(r.ux, f), ay = lane_f32(r.uy, f), az = lane_f32(r.uz, f);
+    // squared spreads reduced, one square root on the maxima (sqrt is monotonic: the same rho as the max
+    // of per-lane roots, with two transcendental instructions per lane fewer)
     float dp = 0.0f, du = 0.0f;
     if (on) {
         const float px = r.px - ox, py = r.py - oy, pz = r.pz - oz;
         const float ux = r.ux - ax, uy = r.uy - ay, uz = r.uz - az;
-        dp = inf_if_nan(sqrtf(fmaf(px, px, fmaf(py, py, pz * pz))));
-        du = inf_if_nan(sqrtf(fmaf(ux, ux, fmaf(uy, uy, uz * uz))));
+        dp = inf_if_nan(fmaf(px, px, fmaf(py, py, pz * pz)));
+        du = inf_if_nan(fmaf(ux, ux, fmaf(uy, uy, uz * uz)));
     }
-    const float rho_o = wave_max(dp), rho_d = wave_max(du);
+    const float rho_o = sqrtf(wave_max(dp)), rho_d = sqrtf(wave_max(du));
     if (!(rho_d < 1.0f) || !(rho_o < 1e30f)) return ~0ull;   // spread too wide: no culling
     bool keep = false;
     if (lane < V.np) {
@@ -785,9 +787,9 @@ __device__ __forceinline__ uint64_t shadow_bundle_mask(const SceneView& V, bool 
     float du = 0.0f;
     if (on) {
         const float ux = r.ux - ax, uy = r.uy - ay, uz = r.uz - az;
-        du = inf_if_nan(sqrtf(fmaf(ux, ux, fmaf(uy, uy, uz * uz))));
+        du = inf_if_nan(fmaf(ux, ux, fmaf(uy, uy, uz * uz)));      // squared (see ray_bundle_mask)
     }
-    const float rho = wave_max(du);
+    const float rho = sqrtf(wave_max(du));
     if (!(rho < 1.0f)) return ~0ull;
     bool keep = false;
     if (lane < V.np) {

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""In-process, interleaved A/B of library builds: the in-tree lib/librt_amd.so ("base") and every
+tools/_var/<name>/librt_amd.so, each loaded as its own handle (copied to a private path) in ONE process, with
+their renders interleaved round by round — so box-to-box and process-to-process clock differences (±2% at c2)
+cancel out.
+
+usage: ab_libs.py [c2,c3,c5] [rounds]        prints one JSON line per (config, lib): median / min kernel ms
+"""
+import ctypes
+import glob
+import json
+import os
+import shutil
+import statistics
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from ray_tracer_fragment_shader_amd import abi, scenes  # noqa: E402
+
+
+def load(path, tmp, name):
+    dst = os.path.join(tmp, f"librt_{name}.so")
+    shutil.copy(path, dst)
+    L = ctypes.CDLL(dst)
+    for fn, (res, args) in abi.SIGNATURES.items():
+        if hasattr(L, fn):
+            getattr(L, fn).restype = res
+            getattr(L, fn).argtypes = args
+    return L
+
+
+def main():
+    cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c2", "c3", "c5"]
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 9
+    reps = int(os.environ.get("REPS", "20"))
+    tmp = tempfile.mkdtemp()
+    libs = {"base": load(abi.LIB_PATH, tmp, "base")}
+    for d in sorted(glob.glob(os.path.join(ROOT, "tools", "_var", "*", "librt_amd.so"))):
+        name = os.path.basename(os.path.dirname(d))
+        libs[name] = load(d, tmp, name)
+    st = torch.cuda.current_stream()
+    ctxs, bufs = {}, {}
+    for name, L in libs.items():
+        c = ctypes.c_void_p()
+        abi.check(L.rt_ctx_create(0, ctypes.byref(c)), "rt_ctx_create")
+        ctxs[name] = c
+    res = {(c, n): [] for c in cfgs for n in libs}
+    for c in cfgs:
+        cfg = scenes.CONFIGS[c]
+        bufs[c] = (torch.empty((cfg.height, cfg.width, 4), dtype=torch.float32, device="cuda"),
+                   torch.empty((cfg.height, cfg.width, 4), dtype=torch.uint8, device="cuda"))
+    for r in range(rounds + 1):                       # round 0: untimed warm-up / calibration / clock settle
+        for c in cfgs:
+            cfg = scenes.CONFIGS[c]
+            sa = cfg.scene().to_abi()
+            cam = cfg.camera()
+            b32, b8 = bufs[c]
+            for name, L in libs.items():
+                abi.check(L.rt_set_scene(ctxs[name], ctypes.byref(sa)), "rt_set_scene")
+                la = (ctxs[name], ctypes.byref(cam), cfg.width, cfg.height, cfg.depth, None,
+                      ctypes.c_void_p(b32.data_ptr()), ctypes.c_void_p(b8.data_ptr()), None, None,
+                      ctypes.c_void_p(st.cuda_stream))
+                for _ in range(3 if r else 40):
+                    abi.check(L.rt_render_dev(*la), "rt_render_dev")
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    L.rt_render_dev(*la)
+                e1.record()
+                torch.cuda.synchronize()
+                if r:
+                    res[(c, name)].append(e0.elapsed_time(e1) / reps)
+    for (c, name), v in res.items():
+        base = statistics.median(res[(c, "base")])
+        med = statistics.median(v)
+        print(json.dumps({"config": c, "lib": name, "median_ms": round(med, 4), "min_ms": round(min(v), 4),
+                          "vs_base": round(med / base - 1, 4)}))
+    for name, L in libs.items():
+        L.rt_ctx_destroy(ctxs[name])
+
+
+if __name__ == "__main__":
+    main()
