@@ -64,9 +64,10 @@
 #ifndef RT_SELF_SKIP
 #define RT_SELF_SKIP 1
 #endif
-// 1: the skips also in the fast (non-CULL) bounce loop; 0: only in the CULL variant.
+// 1: the skips also in the fast (non-CULL) bounce loop; 0 (default): only in the CULL variant — in the fast
+// loop at 6 waves/SIMD the extra live state spilled 12 B/lane (c2 HBM writes 1.01x -> 1.22x algorithmic).
 #ifndef RT_SKIP_FAST
-#define RT_SKIP_FAST 1
+#define RT_SKIP_FAST 0
 #endif
 
 namespace rt {
