@@ -29,6 +29,12 @@ int rt_probe_math_dev(int op, const double* in, int n, double* out, void* stream
  * tile is traced once, by the same code).  RT_EINVAL for another mode. */
 int rt_diag_tile_order(rt_ctx* ctx, int mode);
 
+/* Registers per work-item (*vgprs) and private scratch bytes per work-item (*scratch_bytes) of the render
+ * kernel instance rt_render_dev launches for `depth` (0..7) and scene kind `variant`: 0 spheres + board,
+ * 1 >= 16 spheres (wave-culling variant), 2 meshes or transparent materials, 3 ray trees (whose node stack
+ * lives in scratch by design).  Needs a HIP device.  RT_EINVAL for bad arguments. */
+int rt_diag_kernel_resources(int depth, int variant, int* vgprs, int* scratch_bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -140,9 +140,10 @@ SIGNATURES = {
     # include/rt_diag.h
     "rt_probe_math_dev": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "rt_diag_tile_order": (c_int, [c_void_p, c_int]),
+    "rt_diag_kernel_resources": (c_int, [c_int, c_int, _P(c_int), _P(c_int)]),
 }
 
-_DIAG = {"rt_diag_tile_order"}
+_DIAG = {"rt_diag_tile_order", "rt_diag_kernel_resources"}
 _lib = None
 
 

@@ -995,6 +995,45 @@ extern "C" int rt_diag_tile_order(rt_ctx* c, int mode) {
     return RT_OK;
 }
 
+// Diagnostics (include/rt_diag.h): registers and scratch of the render kernel instance rt_render_dev
+// launches for `depth` and scene kind `variant` (0 spheres + board, 1 >= kConeMin spheres (CULL),
+// 2 meshes / transparency, 3 ray trees) — the tests assert the default instances never spill.
+template <int B>
+static const void* render_kernel_of(int variant) {
+    constexpr int kFast = B <= 3 ? (RT_MINW != 0 ? RT_MINW : (B <= 2 ? 6 : 5)) : 1;
+    constexpr int kCull = B <= 3 ? RT_MINW_CULL : 1;
+    switch (variant) {
+        case 0: return (const void*)rt_render_kernel<B, 0, kFast, false, false, RT_WG_FAST, false>;
+        case 1: return (const void*)rt_render_kernel<B, 0, kCull, false, true, RT_WG_FAST, false>;
+        case 2: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, false>;
+        case 3: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, true>;
+        default: return nullptr;
+    }
+}
+
+extern "C" int rt_diag_kernel_resources(int depth, int variant, int* vgprs, int* scratch_bytes) {
+    if (depth < 0 || depth > RT_MAX_B || variant < 0 || variant > 3 || !vgprs || !scratch_bytes)
+        return rt_fail(RT_EINVAL, "rt_diag_kernel_resources: bad arguments");
+    const void* f = nullptr;
+    switch (depth) {
+        case 0: f = render_kernel_of<0>(variant); break;
+        case 1: f = render_kernel_of<1>(variant); break;
+        case 2: f = render_kernel_of<2>(variant); break;
+        case 3: f = render_kernel_of<3>(variant); break;
+#if RT_MAX_B >= 7
+        case 4: f = render_kernel_of<4>(variant); break;
+        case 5: f = render_kernel_of<5>(variant); break;
+        case 6: f = render_kernel_of<6>(variant); break;
+        case 7: f = render_kernel_of<7>(variant); break;
+#endif
+    }
+    hipFuncAttributes a;
+    RT_HIP(hipFuncGetAttributes(&a, f));
+    *vgprs = a.numRegs;
+    *scratch_bytes = (int)a.localSizeBytes;
+    return RT_OK;
+}
+
 extern "C" int rt_probe_math_dev(int op, const double* in, int n, double* out, void* stream) {
     if (op != 0 && op != 1) return rt_fail(RT_EINVAL, "rt_probe_math_dev: unknown op");
     if (n < 0 || (n > 0 && (!in || !out))) return rt_fail(RT_EINVAL, "rt_probe_math_dev: bad buffers");
