@@ -56,6 +56,11 @@
 #ifndef RT_KEEP_NU
 #define RT_KEEP_NU 0
 #endif
+// The fast loop parks the continuation's end - start in the level's (still empty) LDS colour slot while
+// the light loop runs (fewer live registers) and reloads it for the next ray: at depth >= RT_PARK_ND_MIN_B.
+#ifndef RT_PARK_ND_MIN_B
+#define RT_PARK_ND_MIN_B RT_SKIP_FAST_MIN_B
+#endif
 // 1: rays that start at a board hit skip the board test, rays that start at a sphere hit that sphere's test
 // (certain misses, origin_skip).
 #ifndef RT_BOARD_SKIP
@@ -64,10 +69,12 @@
 #ifndef RT_SELF_SKIP
 #define RT_SELF_SKIP 1
 #endif
-// 1: the skips also in the fast (non-CULL) bounce loop; 0 (default): only in the CULL variant — in the fast
-// loop at 6 waves/SIMD the extra live state spilled 12 B/lane (c2 HBM writes 1.01x -> 1.22x algorithmic).
-#ifndef RT_SKIP_FAST
-#define RT_SKIP_FAST 0
+// The skips in the fast (non-CULL) bounce loop from this depth on (they always run in the CULL variant).
+// There they come with the continuation parked in LDS across the light loop (RT_PARK_ND): without it the
+// extra live state spilled 12 B/lane at 6 waves/SIMD (c2 HBM writes 1.01x -> 1.22x); with it no spills,
+// c3 (depth 2) -1.2 to -1.9%, c2 (depth 1) +0.7 to +1.1% (in-process A/B) — hence depth >= 2.
+#ifndef RT_SKIP_FAST_MIN_B
+#define RT_SKIP_FAST_MIN_B 2
 #endif
 
 namespace rt {
@@ -1068,6 +1075,8 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
     set_dir(&r, d, unit(d));
     uint32_t nseg = 0, nsh = 0;
     int skip = -1;                                          // origin_skip of r's origin
+    constexpr bool kSkip = !TRANSP && B >= RT_SKIP_FAST_MIN_B;  // fast loop: origin skips from this depth
+    constexpr bool kPark = B >= RT_PARK_ND_MIN_B;
 #pragma unroll
     for (int lvl = 0; lvl <= B; ++lvl) {
         const bool alive = lvl == 0 || levels == lvl;
@@ -1090,7 +1099,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                 }
             }
             const bool hit = kind >= 0;
-            skip = (TRANSP || !RT_SKIP_FAST) ? -1 : origin_skip(V, kind, r.p0, p);   // this hit's rays start at p
+            skip = kSkip ? origin_skip(V, kind, r.p0, p) : -1;   // this hit's rays start at p
             d3 nd = mk(0.0, 0.0, 0.0);
 #if RT_KEEP_NU
             d3 nu = nd;
@@ -1106,7 +1115,18 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
 #if RT_KEEP_NU
                 nu = (TRANSP && V.S->mat[mat].transmit) ? unit(nd) : rdir;
 #endif
+                double* psl = slot + 3 * lvl * SS;          // this level's colour slot, written after shade
+                if (kPark && lvl < B) {
+                    psl[0] = nd.x;
+                    psl[SS] = nd.y;
+                    psl[2 * SS] = nd.z;
+                    asm volatile("" ::: "memory");          // keep it in LDS across the light loop
+                }
                 const d3 c = shade<TRANSP, false>(V, true, p, n, mat, ks, skip);
+                if (kPark && lvl < B) {
+                    asm volatile("" ::: "memory");
+                    nd = mk(psl[0], psl[SS], psl[2 * SS]);
+                }
                 park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
                 nsh += V.nl;
                 levels = lvl + 1;
