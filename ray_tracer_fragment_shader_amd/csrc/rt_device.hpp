@@ -56,6 +56,11 @@
 #ifndef RT_KEEP_NU
 #define RT_KEEP_NU 0
 #endif
+// 1: the fast loop also parks the continuation's unit direction (computed before the light loop) in the
+// next level's LDS slot instead of recomputing it after the light loop (RT_KEEP_NU without the registers).
+#ifndef RT_PARK_NU
+#define RT_PARK_NU 1
+#endif
 // The fast loop parks the continuation's end - start in the level's (still empty) LDS colour slot while
 // the light loop runs (fewer live registers) and reloads it for the next ray: at depth >= RT_PARK_ND_MIN_B.
 #ifndef RT_PARK_ND_MIN_B
@@ -1101,7 +1106,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
             const bool hit = kind >= 0;
             skip = kSkip ? origin_skip(V, kind, r.p0, p) : -1;   // this hit's rays start at p
             d3 nd = mk(0.0, 0.0, 0.0);
-#if RT_KEEP_NU
+#if RT_KEEP_NU || RT_PARK_NU
             d3 nu = nd;
 #endif
             if (hit) {
@@ -1112,26 +1117,40 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                 const d3 rdir = unit(rd);                   // reflectedRay.direction()
                 const double ks = fabs(dot(r.u, rdir));     // |u . reflectedRay.direction()|
                 nd = continuation<TRANSP>(V, kind, mat, p, n, r.u, rd);
-#if RT_KEEP_NU
+#if RT_KEEP_NU && !RT_PARK_NU
                 nu = (TRANSP && V.S->mat[mat].transmit) ? unit(nd) : rdir;
 #endif
                 double* psl = slot + 3 * lvl * SS;          // this level's colour slot, written after shade
-                if (kPark && lvl < B) {
+#if RT_PARK_NU
+                // ... and the continuation's unit direction in the next level's slot (written after that
+                // level's shade): no recomputation of unit(nd) after the light loop, no live registers
+                if (lvl < B) {
+                    const d3 nu = (TRANSP && V.S->mat[mat].transmit) ? unit(nd) : rdir;
+                    double* nsl = psl + 3 * SS;
+                    nsl[0] = nu.x;
+                    nsl[SS] = nu.y;
+                    nsl[2 * SS] = nu.z;
+                }
+#endif
+                if ((kPark || RT_PARK_NU) && lvl < B) {
                     psl[0] = nd.x;
                     psl[SS] = nd.y;
                     psl[2 * SS] = nd.z;
                     asm volatile("" ::: "memory");          // keep it in LDS across the light loop
                 }
                 const d3 c = shade<TRANSP, false>(V, true, p, n, mat, ks, skip);
-                if (kPark && lvl < B) {
+                if ((kPark || RT_PARK_NU) && lvl < B) {
                     asm volatile("" ::: "memory");
                     nd = mk(psl[0], psl[SS], psl[2 * SS]);
+#if RT_PARK_NU
+                    nu = mk(psl[3 * SS], psl[4 * SS], psl[5 * SS]);
+#endif
                 }
                 park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
                 nsh += V.nl;
                 levels = lvl + 1;
             }
-#if RT_KEEP_NU
+#if RT_KEEP_NU || RT_PARK_NU
             if (lvl < B) next_ray(p, nd, nu, &r);
 #else
             if (lvl < B) next_ray(hit, p, nd, &r);
