@@ -61,6 +61,10 @@
 #ifndef RT_PARK_NU
 #define RT_PARK_NU 1
 #endif
+// The same for the CULL variant's levels (and its end - start, in this level's slot).
+#ifndef RT_PARK_NU_CULL
+#define RT_PARK_NU_CULL 1
+#endif
 // The fast loop parks the continuation's end - start in the level's (still empty) LDS colour slot while
 // the light loop runs (fewer live registers) and reloads it for the next ray: at depth >= RT_PARK_ND_MIN_B.
 #ifndef RT_PARK_ND_MIN_B
@@ -1052,20 +1056,45 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     d3 n = mk(0.0, 0.0, 0.0), nd = n;
     int mat = 0;
     double ks = 0.0;
+    // (depth >= 3 only: at depth 2 the register allocation of this variant came out worse, 96 VGPRs + spills)
+    constexpr bool kParkCull = RT_PARK_NU_CULL && B >= 3;
+    double* psl = slot + 3 * lvl * SS;                      // this level's colour slot, written after shade
     if (hit) {
         d3 pe;
         surface(V, kind, p, r->u, &n, &mat, &pe);
         const d3 rd = sub(pe, p);                           // reflectedRay = Line(p, p + r)
-        ks = fabs(dot(r->u, unit(rd)));                     // |u . reflectedRay.direction()|
+        const d3 rdir = unit(rd);                           // reflectedRay.direction()
+        ks = fabs(dot(r->u, rdir));                         // |u . reflectedRay.direction()|
         nd = continuation<TRANSP>(V, kind, mat, p, n, r->u, rd);
+        if (kParkCull && lvl < B) {
+            // the continuation (end - start and unit direction) waits in this and the next level's LDS
+            // slots across the light loop: no registers, no unit() after it (as in the fast loop)
+            const d3 nu = (TRANSP && V.S->mat[mat].transmit) ? unit(nd) : rdir;
+            psl[0] = nd.x;
+            psl[SS] = nd.y;
+            psl[2 * SS] = nd.z;
+            psl[3 * SS] = nu.x;
+            psl[4 * SS] = nu.y;
+            psl[5 * SS] = nu.z;
+            asm volatile("" ::: "memory");
+        }
     }
     const d3 c = shade<TRANSP, true>(V, hit, p, n, mat, ks, *skip);
+    d3 nu = nd;
     if (hit) {
+        if (kParkCull && lvl < B) {
+            asm volatile("" ::: "memory");
+            nd = mk(psl[0], psl[SS], psl[2 * SS]);
+            nu = mk(psl[3 * SS], psl[4 * SS], psl[5 * SS]);
+        }
         park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
         *nsh += V.nl;
         *levels = lvl + 1;
     }
-    if (lvl < B) next_ray(hit, p, nd, r);
+    if (lvl < B) {
+        if (kParkCull) next_ray(p, nd, nu, r);
+        else next_ray(hit, p, nd, r);
+    }
     return true;
 }
 
