@@ -70,6 +70,11 @@
 #ifndef RT_PARK_ND_MIN_B
 #define RT_PARK_ND_MIN_B RT_SKIP_FAST_MIN_B
 #endif
+// 1: rays that start at a hit point skip the bounding-sphere cull when the host proved every hit point
+// lies inside its shortcut radius (DevScene::hits_inside).
+#ifndef RT_HITS_INSIDE
+#define RT_HITS_INSIDE 1
+#endif
 // 1: rays that start at a board hit skip the board test, rays that start at a sphere hit that sphere's test
 // (certain misses, origin_skip).
 #ifndef RT_BOARD_SKIP
@@ -553,11 +558,12 @@ __device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const R
 // `mask` (np >= kConeMin): spheres k < 64 this wave's rays may hit (ray_bundle_mask); the rest of the
 // first 64 are skipped.  Spheres are visited in increasing k either way.
 // skip = origin_skip of r's origin: 0 skips the board test, 1 + k sphere k's (certain misses).
+// from_hit: r starts at a hit point, which passes the cull when S->hits_inside (host-proven).
 template <bool FULL, bool CULL = false>
 __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3* hp, uint64_t mask = ~0ull,
-                                           int skip = -1) {
+                                           int skip = -1, bool from_hit = false) {
     const DevScene* S = V.S;
-    if (!bound_pass(S, r.p0, r.u)) return -1;
+    if (!(RT_HITS_INSIDE && from_hit && S->hits_inside) && !bound_pass(S, r.p0, r.u)) return -1;
     int kind = -1;
     double best = -1.0;
     if (S->has_board && skip != 0) {
@@ -833,7 +839,7 @@ template <bool FULL, bool CULL = false>
 __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull,
                                          int skip = -1) {
     const DevScene* S = V.S;
-    if (!bound_pass(S, r.p0, r.u)) return false;
+    if (!(RT_HITS_INSIDE && S->hits_inside) && !bound_pass(S, r.p0, r.u)) return false;   // shadow rays start at hits
     const double eps = S->eps;
     const DevSphereLightF* lf = V.lightf + li * V.np;
     int k0 = 0;
@@ -910,7 +916,7 @@ __device__ __forceinline__ int material_of(const SceneView& V, int kind, d3 p) {
 // Shadow test when some material is transparent: the closest blocker decides (:1219-1221).
 __device__ __forceinline__ bool occluded_transparent(const SceneView& V, const Ray& r) {
     d3 p;
-    int kind = closest_hit<true>(V, r, &p);
+    int kind = closest_hit<true>(V, r, &p, ~0ull, -1, true);        // shadow rays start at hits
     if (kind < 0) return false;
     return V.S->mat[material_of(V, kind, p)].transparent == 0;
 }
@@ -1048,7 +1054,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     if (alive) {
         ++*nseg;
         kind = first ? closest_hit_primary<TRANSP>(V, *r, bdP, bdd, cone, &p)
-                     : closest_hit<TRANSP, true>(V, *r, &p, smask, TRANSP ? -1 : *skip);
+                     : closest_hit<TRANSP, true>(V, *r, &p, smask, TRANSP ? -1 : *skip, lvl > 0);
     }
     const bool hit = kind >= 0;
     *skip = TRANSP ? -1 : origin_skip(V, kind, r->p0, p);      // this hit's rays start at p
@@ -1129,7 +1135,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                     kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p);
                 } else {
                     set_origin_f32(S, &r);
-                    kind = closest_hit<TRANSP>(V, r, &p, ~0ull, TRANSP ? -1 : skip);
+                    kind = closest_hit<TRANSP>(V, r, &p, ~0ull, TRANSP ? -1 : skip, lvl > 0);
                 }
             }
             const bool hit = kind >= 0;

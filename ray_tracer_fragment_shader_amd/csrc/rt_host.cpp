@@ -409,6 +409,7 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     for (int m = 0; m < 5; ++m) d->mat[m] = dm[m];
     d->transparent = any_transparent ? 1 : 0;
     d->tree = tree ? 1 : 0;
+    d->hits_inside = 0;                  // set below, once every object's extent is known
     d->n_lights = s->n_lights;
     for (int k = 0; k < s->n_lights; ++k) {
         for (int q = 0; q < 3; ++q) {
@@ -540,6 +541,25 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
             T.fast = const_quotient_ok(den);
             T.degenerate = degenerate ? 1.0 : 0.0;
         }
+    }
+    // Rays that start at a hit point pass g_scene's bounding-sphere cull when every hit point lies within
+    // R - 1 of its centre (the kernel's bound_pass shortcut, rt_device.hpp): an upper bound of |q - bc| over
+    // the spheres (|C - bc| + r), the board's corners and the meshes' bounding spheres, with a margin far
+    // above the rounding of the hit points, lets the kernel skip the test for them (hits_inside).
+    if (d->bound_on && d->inner2 > 0) {
+        double far = 0.0;
+        for (int k = 0; k < s->n_spheres; ++k)
+            far = std::max(far, length(hp(sph[k].c[0], sph[k].c[1], sph[k].c[2]) - bc) + std::fabs(s->spheres[k].radius));
+        if (d->has_board) {
+            const double h = s->board_half_size;
+            const HP quad = hp(s->board_position) + bc;
+            for (int cx = -1; cx <= 1; cx += 2)
+                for (int cz = -1; cz <= 1; cz += 2) far = std::max(far, length(quad + hp(cx * h, 0, cz * h) - bc));
+        }
+        for (int m = 0; m < s->n_meshes; ++m)
+            far = std::max(far, length(hp(dmesh[m].bc[0], dmesh[m].bc[1], dmesh[m].bc[2]) - bc) + std::sqrt(dmesh[m].br2));
+        const double margin = 1e-6 * (1.0 + far);
+        if (std::isfinite(far) && (far + margin) * (far + margin) < d->inner2 * (1.0 - 1e-9)) d->hits_inside = 1;
     }
     return RT_OK;
 }

@@ -122,6 +122,8 @@ struct alignas(16) DevScene {
     int32_t n_tris;
     int32_t transparent;               // some material is transparent: closest-hit shadows, weighted children
     int32_t tree;                      // some material transmits AND reflects: ray-tree kernels (trace_tree)
+    int32_t hits_inside;               // every hit point lies within (R - 1) of bc: rays from hits pass the cull
+    int32_t pad1;
     DevTri tri[2];                     // board triangles T1 = (P1,P2,P3), T2 = (P1,P3,P4)   (:840-841)
     DevMat mat[5];                     // 0 white square, 1 black square, 2 sphere, 3 tetrahedron, 4 cube
     DevLight light[16];
