@@ -133,6 +133,26 @@ def kernel_rooflines(cfg_name, nl, W, H, avg_kern_ms):
              "reference_flops_per_launch": ref_flops})
 
 
+ROCPROF_ONE_STREAM = "profiles/r03/{cfg}_kernel_stats_1stream.csv"
+
+
+def rocprof_reference(cfg_name, full_frame):
+    """The committed one-stream rocprofv3 --kernel-trace --stats summary of this config (tools/gpu_prof_1stream.sh:
+    bench.py --frames-in-flight 1 --profile-kernel-only): AverageNs of rt_render_kernel is the launch duration,
+    so bytes / AverageNs / peak reproduces `frac` from profiles/ alone."""
+    path = os.path.join(ROOT, ROCPROF_ONE_STREAM.format(cfg=cfg_name))
+    if not full_frame or not os.path.exists(path):
+        return None
+    import csv
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row.get("Name", "").startswith("void rtk::rt_render_kernel") or "rt_render_kernel" in row.get("Name", ""):
+                avg_us = float(row["AverageNs"]) / 1e3
+                return {"rocprof_avg_us": round(avg_us, 3), "rocprof_calls": int(row["Calls"]),
+                        "rocprof_source": ROCPROF_ONE_STREAM.format(cfg=cfg_name)}
+    return None
+
+
 def pipelined_frames(torch, L, abi, trs, sts, launch_args, steps, settle_s):
     """Untimed settle, then `steps` frames round-robin over the streams `sts` (launch_args[i] on sts[i]).
     Returns (wall seconds, per-frame interval in ms from HIP events bracketing all streams)."""
@@ -175,6 +195,76 @@ def serial_kernel_ms(torch, L, abi, launch, stream, n=20):
     e[1].record(stream)
     torch.cuda.synchronize()
     return e[0].elapsed_time(e[1]) / n
+
+
+def packed_host_legs(t, sa, cam, W, H, B, k=30):
+    """draw()'s host frame in the narrowest exact format (rt_render_packed, GRAY8 for the achromatic c2 scene:
+    2.1 MB over PCIe instead of 8.3 MB), synchronous and pipelined (rt_render_packed_async + rt_ctx_wait: the copy of
+    frame k overlaps the render of frame k+1), into pinned memory from rt_host_alloc."""
+    import ctypes
+
+    from ray_tracer_fragment_shader_amd import abi
+    L = abi.lib()
+    pins = []
+    for _ in range(2):
+        p = ctypes.c_void_p()
+        abi.check(L.rt_host_alloc(W * H, ctypes.byref(p)), "rt_host_alloc")
+        pins.append(p)
+    out = {}
+    try:
+        fmt = abi.RT_PIXEL_GRAY8
+        a = (t._ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, B, fmt)
+        for _ in range(3):
+            abi.check(L.rt_render_packed(*a, pins[0], None), "rt_render_packed")
+        t0 = time.perf_counter()
+        for _ in range(k):
+            abi.check(L.rt_render_packed(*a, pins[0], None), "rt_render_packed")
+        out["rt_render_packed_gray8_ms_per_call"] = round((time.perf_counter() - t0) / k * 1e3, 4)
+        tk = [ctypes.c_uint64(), ctypes.c_uint64()]
+        for f in range(4):
+            abi.check(L.rt_render_packed_async(*a, pins[f & 1], ctypes.byref(tk[f & 1])), "rt_render_packed_async")
+        abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
+        t0 = time.perf_counter()
+        for f in range(k):                                  # the draw() loop: queue frame f, show frame f-1
+            abi.check(L.rt_render_packed_async(*a, pins[f & 1], ctypes.byref(tk[f & 1])), "rt_render_packed_async")
+            if f:
+                abi.check(L.rt_ctx_wait(t._ctx, tk[(f - 1) & 1].value), "rt_ctx_wait")
+        abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
+        out["rt_render_packed_async_gray8_ms_per_frame"] = round((time.perf_counter() - t0) / k * 1e3, 4)
+        out["packed_note"] = ("c2 frame as GRAY8 (2.07 MB: the scene is achromatic, rt_scene_achromatic) into pinned "
+                              "memory: synchronous per call, and pipelined (queue frame f, wait for frame f-1: one "
+                              "frame of latency, the copy of f overlaps the render of f+1)")
+    finally:
+        for p in pins:
+            L.rt_host_free(p)
+    return out
+
+
+def dropin_binding_legs(W, H, B, cfg, frames=30):
+    """INTEGRATION.md's C++ binding (lib/rt_dropin: loadScene/draw()/writePpmScreenshot) on the c2 board — light b6,
+    the 8 spheres of SURVEY.md Appendix B — at 1920x1080, pitch 500/W, depth 1: its own 'ms per draw()' over
+    `frames` frames, as the r02 binding ran it (pageable RGBA8) and as it runs now (pinned, auto = GRAY8; and
+    pipelined)."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "ray_tracer_fragment_shader_amd", "lib", "rt_dropin")
+    entries = ["b6:a"] + [f"{sq}:d" for sq in ("d7", "b2", "f5", "h8", "c4", "e2", "g6", "a5")]
+    res = {}
+    with tempfile.TemporaryDirectory() as td:
+        for name, opts in (("pageable_rgba8", ["--pageable", "--format", "rgba"]), ("pinned_auto", []),
+                           ("pinned_auto_pipelined", ["--pipelined"])):
+            cmd = [exe, "--frames", str(frames), "--width", str(W), "--height", str(H), "--pitch", repr(500.0 / W),
+                   "--depth", str(B), "--out", os.path.join(td, "f.ppm")] + opts + entries
+            try:
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+                line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr.strip()
+                ms = float(line.split(" ms per draw()")[0].rsplit(" ", 1)[1]) if r.returncode == 0 else None
+                res[name] = {"ms_per_draw": ms, "output": line}
+            except Exception as exc:                        # reported, the timed metric stands
+                res[name] = {"error": f"{type(exc).__name__}: {exc}"}
+    res["note"] = (f"lib/rt_dropin --frames {frames} (the committed INTEGRATION.md binding, C++, built against "
+                   "rt_api.h): its own steady-state ms per draw() after the first frame, host to host")
+    return res
 
 
 def main() -> int:
@@ -270,6 +360,19 @@ def main() -> int:
         sync()
         barrier()
         elapsed = max_over_ranks(time.perf_counter() - t0)
+        # per-phase times (HIP events on the group's render / comm streams), in a separate untimed pass so the
+        # events do not perturb the timed one
+        abi.check(L.rt_group_timing(g, 1), "rt_group_timing")
+        for _ in range(min(steps, 32)):
+            abi.check(fn(*argv), "rt_render_multi")
+        st = abi.rt_group_stats()
+        abi.check(L.rt_group_get_stats(g, ctypes.byref(st)), "rt_group_get_stats")
+        torch.cuda.synchronize()
+        barrier()
+        phases = {"render_ms": st.render_ms, "gather_ms": st.gather_ms, "assemble_ms": st.assemble_ms,
+                  "frame_ms": st.frame_ms}
+        phases_max = {k: round(max_over_ranks(v), 5) for k, v in phases.items()}
+        names = {abi.RT_PIXEL_GRAY8: "GRAY8", abi.RT_PIXEL_RGB8: "RGB8", abi.RT_PIXEL_RGBA8: "RGBA8", -1: None}
         parity = None
         if rank == 0:                                      # gathered frame == one-launch frame, every byte
             ref = t.render(cam, W, H, B, rgba32f=False, rgba8=True)["rgba8"]
@@ -278,8 +381,19 @@ def main() -> int:
         rays = frame_rays(t, cam, W, H, B) if rank == 0 else 0
         L.rt_group_destroy(g)
         t.close()
-        return {"ranks": world, "rccl_world": world, "band_height": band.value, "slab_rows": slab.value,
-                "rays_per_frame": rays, "parity": parity}, elapsed
+        info = {"ranks": world, "rccl_world": world, "transport": "RCCL", "band_height": band.value,
+                "slab_rows": slab.value, "rays_per_frame": rays, "parity": parity,
+                "wire_format": names.get(st.wire_byte, st.wire_byte), "payload_bytes_to_rank0": st.payload_bytes,
+                "phases_ms_rank0": {k: round(v, 5) for k, v in phases.items()} if rank == 0 else None,
+                "phases_ms_max_over_ranks": phases_max,
+                "phases_note": "HIP events on each rank's render / comm streams over min(steps, 32) untimed frames: "
+                               "render = rt_render_dev of the rank's bands; gather = from the rank's render end to its "
+                               "ncclSend done (rank > 0) or every ncclRecv done (rank 0; includes waiting for peers); "
+                               "assemble = rank 0's unshuffle + expand into RGBA8; frame = rank 0 render start to "
+                               "assembled image (frames overlap: double-buffered slabs)"}
+        if parity is False:
+            info["error"] = "gathered RGBA8 frame differs from the one-launch frame"
+        return info, elapsed
 
     cfg = scenes.CONFIGS[args.config]
     W, H, B = cfg.width, cfg.height, cfg.depth
@@ -313,6 +427,8 @@ def main() -> int:
         torch.cuda.synchronize()
         avg_kern_ms = kern_serial_ms = e[0].elapsed_time(e[1]) / 20
         nfly = 1
+        if rank == 0 and not info["parity"]:
+            raise SystemExit("parity failure: the gathered RGBA8 frame differs from the one-launch frame")
         parity = f"gathered RGBA8 frame == one-launch frame: {info['parity']}"
         res_extra["group"] = info
     else:
@@ -436,12 +552,22 @@ def main() -> int:
     rays_step = rays_frame * job_frames
     value = rays_step * args.steps / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
-    roof, roof64 = kernel_rooflines(args.config, nl, W, H, avg_kern_ms)
+    # The roofline divides by the kernel's own launch duration: launches back to back on one stream (HIP events
+    # on that stream), the figure a one-stream rocprofv3 kernel trace reports as AverageNs (profiles/).  The
+    # per-frame interval with frames in flight (shorter: a launch fills the previous one's tail) is reported
+    # beside it.
+    launch_ms = kern_serial_ms if kern_serial_ms is not None else avg_kern_ms
+    roof, roof64 = kernel_rooflines(args.config, nl, W, H, launch_ms)
     roof["kernel_ms_serial"] = round(kern_serial_ms, 5) if kern_serial_ms is not None else None
+    roof["interval_ms_in_flight"] = round(avg_kern_ms, 5)
     roof["frames_in_flight"] = nfly
-    roof["kernel_ms_note"] = ("kernel_ms: per-frame interval of rt_render_kernel over the timed region, HIP events "
-                              f"bracketing the {nfly} launch stream(s) (a frame's launch overlaps the previous "
-                              "frame's tail when > 1); kernel_ms_serial: launches back to back on one stream")
+    roof["kernel_ms_note"] = ("kernel_ms = kernel_ms_serial: average duration of rt_render_kernel launched back to "
+                              "back on one stream (HIP events on that stream); interval_ms_in_flight: per-frame "
+                              f"interval over the timed region with {nfly} launch stream(s), HIP events bracketing "
+                              "them (a frame's launch overlaps the previous frame's tail when > 1)")
+    prof = rocprof_reference(args.config, nl == H and world == 1)
+    if prof:
+        roof.update(prof)
     if world > 1:
         roof["traffic"] = None                               # the PMC figures are whole-frame, one GPU
 
@@ -509,7 +635,8 @@ def main() -> int:
                                      "c4 machinery at one rank: c3's 3840x2160 frame through rt_render_multi of a "
                                      "one-rank RCCL group (identity band plan: rendered straight into the image)",
                          "frames": steps4, "ms_per_frame": round(el4 / steps4 * 1e3, 4),
-                         "value": round(info["rays_per_frame"] * steps4 / el4 / 1e6, 3) if rank == 0 else None,
+                         "value": (round(info["rays_per_frame"] * steps4 / el4 / 1e6, 3)
+                                   if rank == 0 and "error" not in info else None),
                          "unit": "Mray/s", "scaling": "strong"})
             res_extra["c4"] = info
         except Exception as exc:                            # reported, the timed metric stands
@@ -543,15 +670,19 @@ def main() -> int:
             kser = serial_kernel_ms(torch, L, abi, la[0], stream, n=max(5, k // 2))
             for tt in ts[1:]:
                 tt.close()
-            r1, r2 = kernel_rooflines(name, c.height, c.width, c.height, kms)
+            r1, r2 = kernel_rooflines(name, c.height, c.width, c.height, kser)
             confs[name] = {"workload": f"{name}: {c.width}x{c.height}, {c.n_spheres} spheres + board, "
                                        f"{c.n_lights} light(s), {c.depth} bounce(s), one GPU",
                            "ms_per_frame": round(wall * 1e3, 4), "value": round(rays / wall / 1e6, 3),
-                           "unit": "Mray/s", "rays_per_frame": rays, "kernel_ms": round(kms, 5),
-                           "kernel_ms_serial": round(kser, 5), "frames_in_flight": nf,
+                           "unit": "Mray/s", "rays_per_frame": rays, "kernel_ms": round(kser, 5),
+                           "kernel_ms_serial": round(kser, 5), "interval_ms_in_flight": round(kms, 5),
+                           "frames_in_flight": nf,
                            "hbm_frac": r1["frac"], "hbm_traffic": r1["traffic"],
                            "algorithmic_bytes": r1["algorithmic_bytes_per_launch"], "fp64_frac": r2["frac"],
                            "fp64_reference_equivalent_tflops": r2["reference_equivalent_tflops"]}
+            prof = rocprof_reference(name, True)
+            if prof:
+                confs[name].update(prof)
             t.close()
         res_extra["configs"] = confs
 
@@ -571,6 +702,8 @@ def main() -> int:
         di["rt_render_ms_per_call"] = round((time.perf_counter() - t0c) / k * 1e3, 4)
         di["rt_render_note"] = ("c2 frame, RGBA8 (8.3 MB) copied to pinned host memory each call; scene upload "
                                 "skipped (unchanged); includes launch, kernel, PCIe copy and synchronisation")
+        di.update(packed_host_legs(t, sa, cam, W, H, B))
+        di["dropin_binding"] = dropin_binding_legs(W, H, B, cfg)
         # moving camera: a new eye every frame (per-eye preparation every frame; the tile-row order of the
         # last calibrated camera, re-timed every 8th frame), frames in flight as in the static leg
         views = []

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 #define RT_OK            0
 #define RT_EINVAL       -1   /* bad argument (null pointer, size, unsupported material, ...) */
@@ -212,6 +212,44 @@ int rt_render_dev(rt_ctx* ctx, const rt_camera* cam, int width, int height, int 
                   const rt_rows* rows, float* rgba32f, uint8_t* rgba8, double* rgb64f,
                   uint32_t* raycount, void* stream);
 
+/* ---- packed pixel formats (ABI 5) --------------------------------------------------------------- */
+/* What a frame's bytes look like in a buffer.  Rows are dense (W * bytes per pixel), j = 0 at the bottom.
+ * GRAY formats hold the R channel only and are accepted only for an ACHROMATIC scene (rt_scene_achromatic):
+ * there R = G = B bit for bit, since every colour term of rayTraceRay (:1223-1226, :1241-1246) is a
+ * component-wise product or sum of equal components, so the packed frame expands back to exactly the RGBA
+ * frame.  They cut the bytes of a frame over PCIe (rt_render_packed: glDrawPixels(..., GL_LUMINANCE, ...))
+ * and over xGMI (rt_render_multi's gather: 1 B/px instead of 4). */
+#define RT_PIXEL_RGBA32F 0      /* float4 (r, g, b, 1), 16 B/px (the rgba32f image of rt_render_dev) */
+#define RT_PIXEL_GRAY32F 1      /* float r, 4 B/px (achromatic scenes) */
+#define RT_PIXEL_RGBA8   2      /* 4 B/px (the rgba8 image of rt_render_dev) */
+#define RT_PIXEL_RGB8    3      /* 3 B/px, glDrawPixels(GL_RGB) / PPM order */
+#define RT_PIXEL_GRAY8   4      /* 1 B/px: the R byte of RGBA8 (achromatic scenes) */
+int rt_pixel_bytes(int format, int* bytes);
+/* *out = 1 when the scene is achromatic: every material term the scene's objects use (ambient, diffuse,
+ * specular, transparency of the board squares when the board is present, of the sphere material when there
+ * are spheres, of the tetrahedron / cube materials when such meshes are present) and every light colour has
+ * three equal components (MySdlApplication.cpp:577, 583-588: the app's board, spheres and tetrahedron are; its
+ * red cube is not).  Host only. */
+int rt_scene_achromatic(const rt_scene* scene, int* out);
+/* rt_render_dev with the float image in `float_format` (RT_PIXEL_RGBA32F / GRAY32F) and the byte image in
+ * `byte_format` (RT_PIXEL_RGBA8 / RGB8 / GRAY8); each image nullable.  Same rules as rt_render_dev. */
+int rt_render_dev_packed(rt_ctx* ctx, const rt_camera* cam, int width, int height, int depth, const rt_rows* rows,
+                         int float_format, void* float_pixels, int byte_format, void* byte_pixels, void* stream);
+/* Host-buffer frames in one format (draw()'s replacement with fewer PCIe bytes).  rt_render_packed is
+ * synchronous (stats nullable, as rt_render).  rt_render_packed_async queues the render and the
+ * device-to-host copy on the context's own streams and returns at once with a ticket; the copy of frame t
+ * overlaps the render of frame t+1 (two device buffers); rt_ctx_wait(ctx, t) returns when frame t's pixels
+ * are in host_pixels (ticket 0: everything queued).  host_pixels must stay valid until then; pinned memory
+ * (rt_host_alloc) makes the copy a true DMA. */
+int rt_render_packed(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, int width, int height, int depth,
+                     int format, void* host_pixels, rt_stats* stats);
+int rt_render_packed_async(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, int width, int height,
+                           int depth, int format, void* host_pixels, uint64_t* ticket);
+int rt_ctx_wait(rt_ctx* ctx, uint64_t ticket);
+/* Pinned (page-locked) host memory for host-buffer frames (hipHostMalloc / hipHostFree). */
+int rt_host_alloc(size_t bytes, void** out);
+int rt_host_free(void* p);
+
 /* ---- reference-faithful rayTraceScreen ------------------------------- */
 /* rayTraceScreen (MySdlApplication.cpp:1251-1324) exactly as the app runs it: the incremental unit-step
  * screen walk from (bottom_x, bottom_y) (cam->pitch is not used: the reference steps by the unit vectors
@@ -254,6 +292,10 @@ int rt_trace_rays_dev(rt_ctx* ctx, const double* starts, const double* ends, int
  * elem_bytes in {1,2,4,8,16,24,32}: bytes per pixel. */
 int rt_unshuffle_dev(const void* gathered, void* image, int width, int height, int elem_bytes,
                      int band_height, int n_ranks, int slab_rows, void* stream);
+/* rt_unshuffle_dev from packed slabs in src_format into an image in dst_format: equal formats (a plain
+ * unshuffle), GRAY8 -> RGBA8, RGB8 -> RGBA8, GRAY32F -> RGBA32F (RT_PIXEL_*). */
+int rt_unpack_dev(const void* gathered, void* image, int width, int height, int src_format, int dst_format,
+                  int band_height, int n_ranks, int slab_rows, void* stream);
 
 /* ---- multi-GPU: one frame's rows split over GPUs, gathered to rank 0 ---- */
 /* A group of ranks: rank r renders the round-robin row bands b = r (mod n_ranks) of every frame into its
@@ -283,18 +325,39 @@ int rt_group_destroy(rt_group* group);
  * *transport: RT_TRANSPORT_RCCL or RT_TRANSPORT_COPY.  Each pointer nullable. */
 int rt_group_info(const rt_group* group, int* n_ranks, int* n_local, int* first_rank, int* transport);
 /* One frame over the whole group.  Every rank calls it with the same camera, size, depth, band_height
- * (0 = auto) and `outputs` (RT_OUT_RGBA32F | RT_OUT_RGBA8: what travels).  On rank 0, rgba32f / rgba8 are
- * device images (width x height, j = 0 bottom) on rank 0's device for the requested outputs, assembled in
- * order on `stream` (a hipStream_t of that device; NULL = default stream); other ranks' pointers are
- * ignored.  Asynchronous: rank 0's image is complete when `stream` reaches this call's work. */
+ * (0 = auto) and `outputs` (RT_OUT_RGBA32F | RT_OUT_RGBA8: the images rank 0 receives).  On rank 0, rgba32f /
+ * rgba8 are device images (width x height, j = 0 bottom) on rank 0's device for the requested outputs,
+ * assembled in order on `stream` (a hipStream_t of that device; NULL = default stream); other ranks' pointers
+ * are ignored.  Asynchronous: rank 0's image is complete when `stream` reaches this call's work.
+ * What travels (the wire formats, rt_group_stats): for an achromatic scene (rt_scene_achromatic, decided by
+ * each rank from its own context's scene — they are the same scene) GRAY8 for RGBA8 and GRAY32F for RGBA32F,
+ * otherwise RGB8 and RGBA32F; rank 0 expands them into its images (rt_unpack_dev), byte for byte the images a
+ * single rt_render_dev writes. */
 int rt_render_multi(rt_group* group, const rt_camera* cam, int width, int height, int depth, int band_height,
                     int outputs, float* rgba32f, uint8_t* rgba8, void* stream);
 /* Wait for the group's own render and gather streams (e.g. before timing on a rank > 0). */
 int rt_group_synchronize(rt_group* group);
+/* Per-phase timing of rt_render_multi (HIP events on the group's streams), for this process's ranks. */
+typedef struct rt_group_stats {
+    int32_t frames;              /* frames timed since rt_group_timing(group, 1) (the last <= 64 are averaged) */
+    int32_t wire_float;          /* RT_PIXEL_* sent for RT_OUT_RGBA32F, -1: not requested (last frame) */
+    int32_t wire_byte;           /* RT_PIXEL_* sent for RT_OUT_RGBA8, -1: not requested (last frame) */
+    int32_t ranks_timed;         /* this process's ranks the means are over */
+    uint64_t payload_bytes;      /* bytes rank 0 receives from the other ranks per frame (last frame) */
+    double render_ms;            /* mean rt_render_dev launch on a rank's render stream */
+    double gather_ms;            /* mean send (rank > 0) / receive of every peer's slab (rank 0), from the
+                                    point the rank's own render is done (it includes waiting for peers) */
+    double assemble_ms;          /* rank 0: unshuffle + expand into the images (0 elsewhere) */
+    double frame_ms;             /* rank 0: its render's start to the assembled image (0 elsewhere) */
+} rt_group_stats;
+/* enable = 1: start recording per-phase events from the next frame on (and clear earlier ones); 0: stop. */
+int rt_group_timing(rt_group* group, int enable);
+/* Synchronizes the group's streams, then fills *stats from the recorded frames. */
+int rt_group_get_stats(rt_group* group, rt_group_stats* stats);
 
 /* ---- output (host) -------------------------------------------------------------------------- */
 /* writePpmScreenshot format (Hw4/ppm.cpp:15-25): "P6 W H 255\n" then RGB rows top-down, from an
- * RGBA8 (or RGB8 when channels == 3) bottom-up image as glReadPixels returns it. */
+ * RGBA8 (or RGB8 when channels == 3, GRAY8 when channels == 1) bottom-up image as glReadPixels returns it. */
 int rt_write_ppm(const char* path, const uint8_t* pixels, int width, int height, int channels);
 
 #ifdef __cplusplus

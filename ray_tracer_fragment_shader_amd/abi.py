@@ -26,9 +26,11 @@ RT_MAX_DEPTH = 7
 RT_RAND_GLIBC, RT_RAND_MSVC = 0, 1
 RT_MESH_TETRAHEDRON = 1
 RT_MESH_CUBE = 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 RT_TRANSPORT_AUTO, RT_TRANSPORT_RCCL, RT_TRANSPORT_COPY = -1, 0, 1
 RT_OUT_RGBA32F, RT_OUT_RGBA8 = 1, 2
+RT_PIXEL_RGBA32F, RT_PIXEL_GRAY32F, RT_PIXEL_RGBA8, RT_PIXEL_RGB8, RT_PIXEL_GRAY8 = 0, 1, 2, 3, 4
+PIXEL_BYTES = {RT_PIXEL_RGBA32F: 16, RT_PIXEL_GRAY32F: 4, RT_PIXEL_RGBA8: 4, RT_PIXEL_RGB8: 3, RT_PIXEL_GRAY8: 1}
 RT_COMM_ID_BYTES = 128
 
 D3 = c_double * 3
@@ -95,6 +97,12 @@ class rt_hit(Structure):
                 ("material", c_int32)]
 
 
+class rt_group_stats(Structure):
+    _fields_ = [("frames", c_int32), ("wire_float", c_int32), ("wire_byte", c_int32), ("ranks_timed", c_int32),
+                ("payload_bytes", c_uint64), ("render_ms", c_double), ("gather_ms", c_double),
+                ("assemble_ms", c_double), ("frame_ms", c_double)]
+
+
 class RtError(RuntimeError):
     def __init__(self, code: int, where: str, msg: str):
         super().__init__(f"{where}: rt error {code}: {msg}")
@@ -137,6 +145,20 @@ SIGNATURES = {
     "rt_render_multi": (c_int, [c_void_p, _P(rt_camera), c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                 c_void_p]),
     "rt_group_synchronize": (c_int, [c_void_p]),
+    "rt_group_timing": (c_int, [c_void_p, c_int]),
+    "rt_group_get_stats": (c_int, [c_void_p, _P(rt_group_stats)]),
+    "rt_pixel_bytes": (c_int, [c_int, _P(c_int)]),
+    "rt_scene_achromatic": (c_int, [_P(rt_scene), _P(c_int)]),
+    "rt_render_dev_packed": (c_int, [c_void_p, _P(rt_camera), c_int, c_int, c_int, _P(rt_rows), c_int, c_void_p,
+                                     c_int, c_void_p, c_void_p]),
+    "rt_render_packed": (c_int, [c_void_p, _P(rt_scene), _P(rt_camera), c_int, c_int, c_int, c_int, c_void_p,
+                                 _P(rt_stats)]),
+    "rt_render_packed_async": (c_int, [c_void_p, _P(rt_scene), _P(rt_camera), c_int, c_int, c_int, c_int, c_void_p,
+                                       _P(c_uint64)]),
+    "rt_ctx_wait": (c_int, [c_void_p, c_uint64]),
+    "rt_host_alloc": (c_int, [ctypes.c_size_t, _P(c_void_p)]),
+    "rt_host_free": (c_int, [c_void_p]),
+    "rt_unpack_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     # include/rt_diag.h
     "rt_probe_math_dev": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "rt_diag_tile_order": (c_int, [c_void_p, c_int]),

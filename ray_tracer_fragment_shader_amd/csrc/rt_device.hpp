@@ -75,6 +75,10 @@
 #ifndef RT_HITS_INSIDE
 #define RT_HITS_INSIDE 1
 #endif
+// A/B only: 0 reads the per-eye flag from the scene header at each use (wrong for ray lists)
+#ifndef RT_HITS_VIEW
+#define RT_HITS_VIEW 1
+#endif
 // 1: rays that start at a board hit skip the board test, rays that start at a sphere hit that sphere's test
 // (certain misses, origin_skip).
 #ifndef RT_BOARD_SKIP
@@ -252,7 +256,17 @@ struct SceneView {
     int np;                          // padded sphere count (wave-uniform)
     int nl;                          // light count (wave-uniform)
     int nm;                          // mesh count (wave-uniform)
+    int hits_ok;                     // rays from this kernel's hit points may skip the bounding-sphere cull
 };
+
+// Whether the hit points of rays from origin p0 (and of every later level) lie inside the bounding-sphere
+// shortcut radius: the host proved that every object lies within R - 1 of bc with a slack that covers the
+// rounding of hit points computed from origins up to sqrt(hits_lim2) away (DevScene::hits_lim2, rt_host.cpp).
+// NaN origins fail the compare.
+__device__ __forceinline__ int hits_ok_from(const DevScene* S, d3 p0) {
+    const double dx = p0.x - S->bc[0], dy = p0.y - S->bc[1], dz = p0.z - S->bc[2];
+    return (S->hits_inside != 0) & (dx * dx + dy * dy + dz * dz <= S->hits_lim2);
+}
 
 // hdr: header copy the kernel reads (LDS or global); g: the global record (for the filter images).
 __device__ __forceinline__ SceneView view_of(const DevScene* hdr, const DevScene* g, int np, int nl) {
@@ -271,6 +285,7 @@ __device__ __forceinline__ SceneView view_of(const DevScene* hdr, const DevScene
     v.mesh = reinterpret_cast<const DevMesh*>(v.lightf + (size_t)nl * np);
     v.nm = g->n_meshes;
     v.tri = reinterpret_cast<const DevTri*>(v.mesh + v.nm);
+    v.hits_ok = hdr->hits_ok;        // for the camera eye (rt_prepare_kernel); ray lists set it per ray
     return v;
 }
 
@@ -563,7 +578,7 @@ template <bool FULL, bool CULL = false>
 __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3* hp, uint64_t mask = ~0ull,
                                            int skip = -1, bool from_hit = false) {
     const DevScene* S = V.S;
-    if (!(RT_HITS_INSIDE && from_hit && S->hits_inside) && !bound_pass(S, r.p0, r.u)) return -1;
+    if (!(RT_HITS_INSIDE && from_hit && (RT_HITS_VIEW ? V.hits_ok : S->hits_ok)) && !bound_pass(S, r.p0, r.u)) return -1;
     int kind = -1;
     double best = -1.0;
     if (S->has_board && skip != 0) {
@@ -839,7 +854,7 @@ template <bool FULL, bool CULL = false>
 __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull,
                                          int skip = -1) {
     const DevScene* S = V.S;
-    if (!(RT_HITS_INSIDE && S->hits_inside) && !bound_pass(S, r.p0, r.u)) return false;   // shadow rays start at hits
+    if (!(RT_HITS_INSIDE && (RT_HITS_VIEW ? V.hits_ok : S->hits_ok)) && !bound_pass(S, r.p0, r.u)) return false;   // shadow rays start at hits
     const double eps = S->eps;
     const DevSphereLightF* lf = V.lightf + li * V.np;
     int k0 = 0;

@@ -15,6 +15,12 @@
 // Stream priorities: rs lowest, cs highest (the gather's kernels do not queue behind the next render grid).
 // A one-rank group renders straight into the caller's image on the caller's stream (identity band plan).
 //
+// What travels: the wire formats.  An achromatic scene (every colour term with R = G = B, rt_scene_achromatic)
+// renders R = G = B bit for bit, so the RGBA8 image travels as GRAY8 (1 B/px) and RGBA32F as GRAY32F (4 B/px);
+// other scenes send RGB8 (3 B/px; alpha is the constant 255) and RGBA32F.  The root expands them into its images
+// in the same kernel that puts the bands in image order (rt_unpack_dev).  At c4 (3840 x 2160 over 8 ranks) the
+// root's ingress is 7/8 of 8.3 MB instead of 7/8 of 33.2 MB.
+//
 // b = frame & 1: the slabs and the root's gather buffer are double-buffered, so frame f's gather overlaps
 // frame f+1's render.  Transports: RCCL (ncclCommInitAll for one process driving n GPUs, ncclCommInitRank
 // for one process per GPU) or COPY (hipMemcpyPeerAsync on the root's comm stream; used when contexts share
@@ -33,8 +39,16 @@
 
 namespace {
 
-constexpr int kKinds = 2;                      // 0: RGBA32F (16 B/px), 1: RGBA8 (4 B/px)
-constexpr size_t kElem[kKinds] = {16, 4};
+constexpr int kKinds = 2;                      // 0: the RGBA32F image, 1: the RGBA8 image
+constexpr int kImageFormat[kKinds] = {RT_PIXEL_RGBA32F, RT_PIXEL_RGBA8};
+constexpr int kRing = 64;                      // frames of per-phase timing events kept
+
+// Per-phase timing events of one frame on one rank (rt_group_timing): render start / end on the render stream,
+// gather start (the rank's render is done) / end on the comm stream, and on the root the assembled image.
+struct PhaseEvents {
+    hipEvent_t r0 = nullptr, r1 = nullptr, g0 = nullptr, g1 = nullptr, a1 = nullptr;
+    bool rec = false, gather_rec = false;
+};
 
 struct Rank {
     rt_ctx* ctx = nullptr;
@@ -47,6 +61,7 @@ struct Rank {
     void* slab[2][kKinds] = {{nullptr, nullptr}, {nullptr, nullptr}};
     size_t slab_cap[2][kKinds] = {{0, 0}, {0, 0}};
     ncclComm_t comm = nullptr;
+    PhaseEvents ph[kRing];
 };
 
 }  // namespace
@@ -64,6 +79,11 @@ struct rt_group {
     bool assembled_rec[2] = {false, false};
     uint64_t frame = 0;
     int last_band = 0, last_slab_rows = 0;
+    // timing (rt_group_timing): frames [t_first, frame) are recorded, the last kRing of them kept
+    bool timing = false;
+    uint64_t t_first = 0;
+    int last_wire[kKinds] = {-1, -1};
+    uint64_t last_payload = 0;
 };
 
 namespace {
@@ -140,6 +160,9 @@ extern "C" int rt_group_destroy(rt_group* g) {
     for (auto& r : g->ranks) {
         (void)hipSetDevice(r.device);
         if (r.comm) (void)ncclCommDestroy(r.comm);
+        for (auto& e : r.ph)
+            for (hipEvent_t ev : {e.r0, e.r1, e.g0, e.g1, e.a1})
+                if (ev) (void)hipEventDestroy(ev);
         for (int b = 0; b < 2; ++b) {
             if (r.rendered[b]) (void)hipEventDestroy(r.rendered[b]);
             if (r.sent[b] && g->transport == RT_TRANSPORT_RCCL) (void)hipEventDestroy(r.sent[b]);
@@ -266,6 +289,74 @@ extern "C" int rt_group_synchronize(rt_group* g) {
     return RT_OK;
 }
 
+// Timing events of ring slot `slot` for rank r, created on its device on first use.
+int phase_events(Rank& r, int slot, bool root, PhaseEvents** out) {
+    PhaseEvents& e = r.ph[slot];
+    if (!e.r0) {
+        G_HIP(hipSetDevice(r.device));
+        for (hipEvent_t* ev : {&e.r0, &e.r1, &e.g0, &e.g1}) G_HIP(hipEventCreate(ev));
+        if (root) G_HIP(hipEventCreate(&e.a1));
+    }
+    *out = &e;
+    return RT_OK;
+}
+
+extern "C" int rt_group_timing(rt_group* g, int enable) {
+    if (!g) return rt_fail(RT_EINVAL, "rt_group_timing: null group");
+    int rc = rt_group_synchronize(g);
+    if (rc) return rc;
+    g->timing = enable != 0;
+    g->t_first = g->frame;
+    for (auto& r : g->ranks)
+        for (auto& e : r.ph) e.rec = e.gather_rec = false;
+    return RT_OK;
+}
+
+extern "C" int rt_group_get_stats(rt_group* g, rt_group_stats* st) {
+    if (!g || !st) return rt_fail(RT_EINVAL, "rt_group_get_stats: null argument");
+    int rc = rt_group_synchronize(g);
+    if (rc) return rc;
+    memset(st, 0, sizeof(*st));
+    st->frames = (int32_t)(g->frame - g->t_first);
+    st->wire_float = g->last_wire[0];
+    st->wire_byte = g->last_wire[1];
+    st->payload_bytes = g->last_payload;
+    double sr = 0, sg = 0, sa = 0, sf = 0;
+    int nr = 0, ng = 0, na = 0;
+    for (size_t q = 0; q < g->ranks.size(); ++q) {
+        Rank& r = g->ranks[q];
+        bool any = false;
+        G_HIP(hipSetDevice(r.device));
+        for (auto& e : r.ph) {
+            if (!e.rec) continue;
+            any = true;
+            // a one-rank group records on the caller's stream, which rt_group_synchronize does not wait for
+            G_HIP(hipEventSynchronize(e.r1));
+            if (e.gather_rec) G_HIP(hipEventSynchronize(e.g1));
+            if (q == 0 && g->owns_root && e.a1) G_HIP(hipEventSynchronize(e.a1));
+            float ms = 0.f;
+            G_HIP(hipEventElapsedTime(&ms, e.r0, e.r1));
+            sr += ms, ++nr;
+            if (e.gather_rec) {
+                G_HIP(hipEventElapsedTime(&ms, e.g0, e.g1));
+                sg += ms, ++ng;
+            }
+            if (q == 0 && g->owns_root && e.a1) {
+                G_HIP(hipEventElapsedTime(&ms, e.g1, e.a1));
+                sa += ms;
+                G_HIP(hipEventElapsedTime(&ms, e.r0, e.a1));
+                sf += ms, ++na;
+            }
+        }
+        st->ranks_timed += any ? 1 : 0;
+    }
+    st->render_ms = nr ? sr / nr : 0.0;
+    st->gather_ms = ng ? sg / ng : 0.0;
+    st->assemble_ms = na ? sa / na : 0.0;
+    st->frame_ms = na ? sf / na : 0.0;
+    return RT_OK;
+}
+
 extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, int depth, int band_height,
                                int outputs, float* rgba32f, uint8_t* rgba8, void* stream) {
     if (!g) return rt_fail(RT_EINVAL, "rt_render_multi: null group");
@@ -282,25 +373,59 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     int rc = rt_band_plan(H, g->n_ranks, band_height, &hb, &slab_rows);
     if (rc) return rc;
     const int b = (int)(g->frame & 1);
+    const int slot = (int)(g->frame % kRing);
     const hipStream_t st = (hipStream_t)stream;
+    // Wire formats: every local rank must see the same scene (each decides from its own context).
+    const int achro = rt_ctx_achromatic(g->ranks[0].ctx);
+    for (auto& r : g->ranks)
+        if (rt_ctx_achromatic(r.ctx) != achro)
+            return rt_fail(RT_EINVAL, "rt_render_multi: the ranks' contexts hold different scenes");
+    const int wire[kKinds] = {achro ? RT_PIXEL_GRAY32F : RT_PIXEL_RGBA32F, achro ? RT_PIXEL_GRAY8 : RT_PIXEL_RGB8};
+    size_t elem[kKinds];
+    for (int k = 0; k < kKinds; ++k) {
+        int pb = 0;
+        rt_pixel_bytes(wire[k], &pb);
+        elem[k] = (size_t)pb;
+        g->last_wire[k] = kind_on[k] ? wire[k] : -1;
+    }
 
     // ---- one rank: the band plan is the identity, so the frame is rendered straight into the caller's image
     // on the caller's stream (no slab, no unshuffle, no cross-stream hand-off: each one costs ~30 us) ----
     if (g->n_ranks == 1) {
         Rank& r = g->ranks[0];
         G_HIP(hipSetDevice(r.device));
+        PhaseEvents* e = nullptr;
+        if (g->timing && (rc = phase_events(r, slot, true, &e))) return rc;
+        if (e) G_HIP(hipEventRecord(e->r0, st));
         rc = rt_render_dev(r.ctx, cam, W, H, depth, nullptr, kind_on[0] ? rgba32f : nullptr,
                            kind_on[1] ? rgba8 : nullptr, nullptr, nullptr, st);
         if (rc) return rc;
+        if (e) {
+            G_HIP(hipSetDevice(r.device));
+            G_HIP(hipEventRecord(e->r1, st));
+            G_HIP(hipEventRecord(e->g1, st));
+            G_HIP(hipEventRecord(e->a1, st));
+            e->rec = true;
+            e->gather_rec = false;
+        }
         g->last_band = hb;
         g->last_slab_rows = slab_rows;
+        g->last_payload = 0;
         ++g->frame;
         return RT_OK;
     }
 
-    // ---- buffers (grow-only; a size change waits for the frames still using them) -----------------------
-    const bool regrow = hb != g->last_band || slab_rows != g->last_slab_rows;
-    if (regrow && g->frame > 0) {
+    // ---- buffers (grow-only).  A buffer that must grow may still be in use by frame - 2 (a peer copy or an RCCL
+    // receive on the root, a send on a rank, the root's unshuffle): wait for the group and the caller's stream
+    // first, whatever changed (width, band plan, outputs, wire format). ----
+    bool must_grow = false;
+    for (auto& r : g->ranks)
+        for (int k = 0; k < kKinds; ++k)
+            must_grow |= kind_on[k] && (size_t)slab_rows * W * elem[k] > r.slab_cap[b][k];
+    if (g->owns_root)
+        for (int k = 0; k < kKinds; ++k)
+            must_grow |= kind_on[k] && (size_t)g->n_ranks * slab_rows * W * elem[k] > g->gathered_cap[b][k];
+    if (must_grow && g->frame > 0) {
         rc = rt_group_synchronize(g);
         if (rc) return rc;
         if (g->owns_root) {
@@ -313,28 +438,35 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     for (auto& r : g->ranks) {
         G_HIP(hipSetDevice(r.device));
         for (int k = 0; k < kKinds; ++k)
-            if (kind_on[k] && (rc = grow(&r.slab[b][k], &r.slab_cap[b][k], (size_t)slab_rows * W * kElem[k])))
+            if (kind_on[k] && (rc = grow(&r.slab[b][k], &r.slab_cap[b][k], (size_t)slab_rows * W * elem[k])))
                 return rc;
     }
     if (g->owns_root) {
         G_HIP(hipSetDevice(g->ranks[0].device));
         for (int k = 0; k < kKinds; ++k)
             if (kind_on[k] && (rc = grow(&g->gathered[b][k], &g->gathered_cap[b][k],
-                                         (size_t)g->n_ranks * slab_rows * W * kElem[k])))
+                                         (size_t)g->n_ranks * slab_rows * W * elem[k])))
                 return rc;
     }
+    std::vector<PhaseEvents*> pe(g->ranks.size(), nullptr);
+    if (g->timing)
+        for (size_t q = 0; q < g->ranks.size(); ++q)
+            if ((rc = phase_events(g->ranks[q], slot, q == 0 && g->owns_root, &pe[q]))) return rc;
 
-    // ---- render: every local rank's bands into slab[b] ------------------------------------------------------
-    for (auto& r : g->ranks) {
+    // ---- render: every local rank's bands into slab[b], in the wire formats ---------------------------------
+    for (size_t q = 0; q < g->ranks.size(); ++q) {
+        Rank& r = g->ranks[q];
         G_HIP(hipSetDevice(r.device));
         if (r.sent_rec[b]) G_HIP(hipStreamWaitEvent(r.rs, r.sent[b], 0));     // slab[b] has left (frame - 2)
         if (r.rank == 0 && g->assembled_rec[b])                               // the root's slab[b] is read by
             G_HIP(hipStreamWaitEvent(r.rs, g->assembled[b], 0));              // frame - 2's unshuffle
+        if (pe[q]) G_HIP(hipEventRecord(pe[q]->r0, r.rs));
         rt_rows rows = {hb, g->n_ranks, r.rank, 1};
-        rc = rt_render_dev(r.ctx, cam, W, H, depth, &rows, (float*)r.slab[b][0], (uint8_t*)r.slab[b][1], nullptr,
-                           nullptr, r.rs);
+        rc = rt_render_dev_packed(r.ctx, cam, W, H, depth, &rows, wire[0], kind_on[0] ? r.slab[b][0] : nullptr,
+                                  wire[1], kind_on[1] ? r.slab[b][1] : nullptr, r.rs);
         if (rc) return rc;
         G_HIP(hipSetDevice(r.device));
+        if (pe[q]) G_HIP(hipEventRecord(pe[q]->r1, r.rs));
         G_HIP(hipEventRecord(r.rendered[b], r.rs));
     }
 
@@ -345,21 +477,28 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         rt_local_rows(H, &rr, &nl);
         return nl;
     };
+    uint64_t payload = 0;
+    for (int q = 1; q < g->n_ranks; ++q)
+        for (int k = 0; k < kKinds; ++k)
+            if (kind_on[k]) payload += (uint64_t)rows_of(q) * W * elem[k];
+    g->last_payload = payload;
     if (g->owns_root) {
         Rank& root = g->ranks[0];
         G_HIP(hipSetDevice(root.device));
         if (g->assembled_rec[b]) G_HIP(hipStreamWaitEvent(root.cs, g->assembled[b], 0));   // gathered[b] is free
     }
     if (g->transport == RT_TRANSPORT_RCCL) {
-        for (auto& r : g->ranks) {
+        for (size_t q = 0; q < g->ranks.size(); ++q) {
+            Rank& r = g->ranks[q];
             G_HIP(hipSetDevice(r.device));
             G_HIP(hipStreamWaitEvent(r.cs, r.rendered[b], 0));
+            if (pe[q]) G_HIP(hipEventRecord(pe[q]->g0, r.cs));
         }
         G_NCCL(ncclGroupStart());
         for (auto& r : g->ranks) {
             for (int k = 0; k < kKinds; ++k) {
                 if (!kind_on[k]) continue;
-                const size_t bytes = (size_t)rows_of(r.rank) * W * kElem[k];
+                const size_t bytes = (size_t)rows_of(r.rank) * W * elem[k];
                 ncclResult_t e = ncclSuccess;
                 if (r.rank != 0) e = ncclSend(r.slab[b][k], bytes, ncclUint8, 0, r.comm, r.cs);
                 if (e != ncclSuccess) {
@@ -368,8 +507,8 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
                 }
                 if (r.rank != 0) continue;
                 for (int q = 1; q < g->n_ranks; ++q) {        // the root's own slab is unshuffled in place
-                    char* dst = (char*)g->gathered[b][k] + (size_t)q * slab_rows * W * kElem[k];
-                    e = ncclRecv(dst, (size_t)rows_of(q) * W * kElem[k], ncclUint8, q, r.comm, r.cs);
+                    char* dst = (char*)g->gathered[b][k] + (size_t)q * slab_rows * W * elem[k];
+                    e = ncclRecv(dst, (size_t)rows_of(q) * W * elem[k], ncclUint8, q, r.comm, r.cs);
                     if (e != ncclSuccess) {
                         (void)ncclGroupEnd();
                         return rt_fail(RT_EHIP, std::string("ncclRecv: ") + ncclGetErrorString(e));
@@ -378,24 +517,36 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
             }
         }
         G_NCCL(ncclGroupEnd());
-        for (auto& r : g->ranks) {
+        for (size_t q = 0; q < g->ranks.size(); ++q) {
+            Rank& r = g->ranks[q];
             G_HIP(hipSetDevice(r.device));
+            if (pe[q]) {
+                G_HIP(hipEventRecord(pe[q]->g1, r.cs));
+                pe[q]->gather_rec = true;
+            }
             G_HIP(hipEventRecord(r.sent[b], r.cs));
             r.sent_rec[b] = true;
         }
     } else {
         Rank& root = g->ranks[0];
         G_HIP(hipSetDevice(root.device));
+        // the root's gather: from its own render's end (as in RCCL mode) to the last peer copy
+        G_HIP(hipStreamWaitEvent(root.cs, root.rendered[b], 0));
+        if (pe[0]) G_HIP(hipEventRecord(pe[0]->g0, root.cs));
         for (auto& r : g->ranks) {
             G_HIP(hipStreamWaitEvent(root.cs, r.rendered[b], 0));
             for (int k = 0; k < kKinds; ++k) {
                 if (!kind_on[k] || r.rank == 0) continue;      // the root's own slab is unshuffled in place
-                char* dst = (char*)g->gathered[b][k] + (size_t)r.rank * slab_rows * W * kElem[k];
+                char* dst = (char*)g->gathered[b][k] + (size_t)r.rank * slab_rows * W * elem[k];
                 G_HIP(hipMemcpyPeerAsync(dst, root.device, r.slab[b][k], r.device,
-                                         (size_t)rows_of(r.rank) * W * kElem[k], root.cs));
+                                         (size_t)rows_of(r.rank) * W * elem[k], root.cs));
             }
             G_HIP(hipEventRecord(r.sent[b], root.cs));
             r.sent_rec[b] = true;
+        }
+        if (pe[0]) {
+            G_HIP(hipEventRecord(pe[0]->g1, root.cs));
+            pe[0]->gather_rec = true;
         }
     }
 
@@ -409,15 +560,18 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         G_HIP(hipStreamWaitEvent(root.cs, g->received[b], 0));
         for (int k = 0; k < kKinds; ++k) {
             if (!kind_on[k]) continue;
-            rc = rt_unshuffle_dev_ex(g->gathered[b][k], root.slab[b][k], outs[k], W, H, (int)kElem[k], hb, g->n_ranks,
-                                     slab_rows, root.cs);
+            rc = rt_unpack_dev_ex(g->gathered[b][k], root.slab[b][k], outs[k], W, H, wire[k], kImageFormat[k], hb,
+                                  g->n_ranks, slab_rows, root.cs);
             if (rc) return rc;
         }
         G_HIP(hipSetDevice(root.device));
+        if (pe[0]) G_HIP(hipEventRecord(pe[0]->a1, root.cs));
         G_HIP(hipEventRecord(g->assembled[b], root.cs));
         G_HIP(hipStreamWaitEvent(st, g->assembled[b], 0));
         g->assembled_rec[b] = true;
     }
+    for (auto* e : pe)
+        if (e) e->rec = true;
     ++g->frame;
     return RT_OK;
 }

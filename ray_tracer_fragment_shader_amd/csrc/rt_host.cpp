@@ -410,6 +410,8 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     d->transparent = any_transparent ? 1 : 0;
     d->tree = tree ? 1 : 0;
     d->hits_inside = 0;                  // set below, once every object's extent is known
+    d->hits_lim2 = -1.0;
+    d->hits_ok = 0;                      // per eye, rt_prepare_kernel
     d->n_lights = s->n_lights;
     for (int k = 0; k < s->n_lights; ++k) {
         for (int q = 0; q < 3; ++q) {
@@ -558,16 +560,57 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
         }
         for (int m = 0; m < s->n_meshes; ++m)
             far = std::max(far, length(hp(dmesh[m].bc[0], dmesh[m].bc[1], dmesh[m].bc[2]) - bc) + std::sqrt(dmesh[m].br2));
-        const double margin = 1e-6 * (1.0 + far);
-        if (std::isfinite(far) && (far + margin) * (far + margin) < d->inner2 * (1.0 - 1e-9)) d->hits_inside = 1;
+        // Hit points carry rounding that grows with their ray's origin o (D = |o - bc|): a sphere hit's
+        // |q - C|^2 = r^2 + err(disc), err(disc) <= 2^-49 D^2 (the sqrt keeps it below 2^-50 D^2 / r in |q - C|),
+        // and p0 + s u or p0 + m d adds <= 2^-51 (D + |bc| + far).  dev(D) = 2^-44 (D + |bc| + far + 1 + D^2 / rmin)
+        // bounds both with room; the shortcut is kept for origins with dev(D) <= slack / 2 (hits_lim2, checked per
+        // ray on the device: the camera eye per render, every start of a ray list), and only when that covers the
+        // hit points themselves (D = R: the origins of later levels).
+        const double Rin = std::sqrt(d->inner2) * (1.0 - 1e-9);
+        const double slack = Rin - far - 1e-6 * (1.0 + far);
+        double rmin = std::numeric_limits<double>::infinity();
+        for (int k = 0; k < s->n_spheres; ++k) rmin = std::min(rmin, std::fabs(s->spheres[k].radius));
+        const double absbc = length(bc);
+        const double e = 0x1p-44, a = rmin > 0 ? e / rmin : inf, c = e * (absbc + far + 1.0) - slack / 2;
+        double dlim = -1.0;                                  // largest D with a D^2 + e D + c <= 0
+        if (std::isfinite(far) && std::isfinite(absbc) && slack > 0 && c < 0)
+            dlim = std::isfinite(a) ? (-e + std::sqrt(e * e - 4 * a * c)) / (2 * a) : -c / e;
+        if (dlim >= Rin) {
+            d->hits_inside = 1;
+            d->hits_lim2 = dlim * dlim * (1.0 - 1e-9);
+        }
     }
+    return RT_OK;
+}
+
+// R = G = B bit for bit in every frame of the scene: rayTraceRay's colour (:1213-1247) is built from the
+// light colours, the material terms and scalar factors by component-wise products and sums only, and every
+// decision (hits, shadows, which continuations, :1221, :1230-1247) is the same for the three channels (it
+// depends on geometry and on "any component != 0" tests), so equal components in every term that enters the
+// sum give equal channels.  Checked: the materials the scene's objects carry and every light colour.
+extern "C" int rt_scene_achromatic(const rt_scene* s, int* out) {
+    if (!s || !out) return rt_fail(RT_EINVAL, "rt_scene_achromatic: null pointer");
+    *out = 0;
+    auto grey = [](const double v[3]) { return v[0] == v[1] && v[1] == v[2]; };
+    auto grey_mat = [&](const rt_material& m) {
+        return grey(m.ambient) && grey(m.diffuse) && grey(m.specular) && grey(m.transparency);
+    };
+    if (s->n_lights > 0 && !s->lights) return rt_fail(RT_EINVAL, "rt_scene_achromatic: null lights");
+    if (s->n_meshes > 0 && !s->meshes) return rt_fail(RT_EINVAL, "rt_scene_achromatic: null meshes");
+    bool ok = true;
+    if (s->has_board) ok = ok && grey_mat(s->white_square) && grey_mat(s->black_square);
+    if (s->n_spheres > 0) ok = ok && grey_mat(s->sphere_material);
+    for (int m = 0; m < s->n_meshes && ok; ++m)
+        ok = grey_mat(s->meshes[m].kind == RT_MESH_TETRAHEDRON ? s->tetrahedron_material : s->cube_material);
+    for (int k = 0; k < s->n_lights && ok; ++k) ok = grey(s->lights[k].color);
+    *out = ok ? 1 : 0;
     return RT_OK;
 }
 
 extern "C" int rt_write_ppm(const char* path, const uint8_t* px, int W, int H, int channels) {
     // writePpmScreenshot (Hw4/ppm.cpp:15-25): header "P6 W H 255\n", then the bottom-up GL image's rows
     // written top-down (image[3*w*(h-1-i)]).
-    if (!path || !px || W <= 0 || H <= 0 || (channels != 3 && channels != 4))
+    if (!path || !px || W <= 0 || H <= 0 || (channels != 1 && channels != 3 && channels != 4))
         return rt_fail(RT_EINVAL, "rt_write_ppm: bad args");
     FILE* f = fopen(path, "wb");
     if (!f) return rt_fail(RT_EINVAL, std::string("rt_write_ppm: cannot open ") + path);
@@ -575,10 +618,10 @@ extern "C" int rt_write_ppm(const char* path, const uint8_t* px, int W, int H, i
     std::vector<unsigned char> row((size_t)W * 3);
     for (int i = 0; i < H; ++i) {
         const uint8_t* src = px + (size_t)(H - 1 - i) * W * channels;
-        for (int x = 0; x < W; ++x) {
+        for (int x = 0; x < W; ++x) {                        // GRAY8 (channels 1): R = G = B
             row[3 * x] = src[channels * x];
-            row[3 * x + 1] = src[channels * x + 1];
-            row[3 * x + 2] = src[channels * x + 2];
+            row[3 * x + 1] = src[channels * x + (channels > 1 ? 1 : 0)];
+            row[3 * x + 2] = src[channels * x + (channels > 1 ? 2 : 0)];
         }
         if (fwrite(row.data(), 1, row.size(), f) != row.size()) {
             fclose(f);

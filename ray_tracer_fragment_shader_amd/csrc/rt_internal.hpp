@@ -20,7 +20,14 @@ void rt_camera_basis(const rt_camera* cam, double right[3], double upp[3]);
 // Device ordinal of a context (rt_group.cpp).
 int rt_ctx_device(const rt_ctx* ctx);
 
+// 1 when the context's uploaded scene is achromatic (rt_scene_achromatic): GRAY pixel formats are exact.
+int rt_ctx_achromatic(const rt_ctx* ctx);
+
 // rt_unshuffle_dev with rank 0's rows read from `rank0_slab` instead of the gathered buffer (the group's root
 // unshuffles its own slab in place of sending it to itself); rank0_slab = nullptr: from `gathered`.
 int rt_unshuffle_dev_ex(const void* gathered, const void* rank0_slab, void* image, int W, int H, int elem_bytes,
                         int band_height, int n_ranks, int slab_rows, void* stream);
+
+// rt_unpack_dev with rank 0's rows read from `rank0_slab` (as rt_unshuffle_dev_ex).
+int rt_unpack_dev_ex(const void* gathered, const void* rank0_slab, void* image, int W, int H, int src_format,
+                     int dst_format, int band_height, int n_ranks, int slab_rows, void* stream);

@@ -1,19 +1,15 @@
 // rt_kernel.hip — MI355X (gfx950) kernels and the device half of the C ABI (include/rt_api.h).
 //
-// Kernels
-//   rt_render_kernel<B, LDS, MINW, TRANSP, CULL, WG>  one work-item per pixel, FP64, iterative bounce loop
-//                             (rt_device.hpp); CULL: wave-level sphere culling for >= kConeMin spheres.
-//                             Default: one-wave workgroups (WG = 64), each owning an 8 x 8 pixel tile
-//                             (square tiles keep a wave's rays coherent, so the __any early-out and the
-//                             culling masks work for whole waves).  The scene (bounding sphere, board,
-//                             materials, lights, spheres) is read through the scalar cache; the A/B
-//                             variants with 256-thread workgroups (32 x 8 tiles) copy it into LDS once per
-//                             workgroup (LDS = 1) or stage the output tile in LDS for 32-pixel row stores.
-//                             Per-level colours wait in LDS slots; stores go out per wave (8 rows of
-//                             128 B of RGBA32F).
-//   rt_trace_rays_kernel<B>   rayTraceRay on an arbitrary ray list (parity / fuzz entry point).
-//   rt_intersect_kernel       g_scene.intersection on an arbitrary ray list (primitive KATs).
-//   rt_unshuffle_kernel       multi-GPU: gathered row bands -> image order.
+// Kernels (the render and ray-list kernels are templates in rt_render.hpp, instantiated per depth in
+// rt_render_b<B>.hip; the rest live here)
+//   rt_render_kernel<...>     one work-item per pixel, FP64, iterative bounce loop (rt_render.hpp)
+//   rt_trace_rays_kernel<B>   rayTraceRay on an arbitrary ray list (rt_render.hpp)
+//   rt_prepare_kernel         per-eye sphere data, board numerator and cull flag (once per camera eye)
+//   rt_scene_init_kernel      device-side reciprocals of constant divisors (once per scene)
+//   rt_order_kernel           longest-first tile-row order from a calibration render
+//   rt_intersect_kernel       g_scene.intersection on an arbitrary ray list (primitive KATs)
+//   rt_unpack_kernel          multi-GPU: gathered row bands -> image order, packed pixels -> RGBA
+//   rt_raysum_kernel          rt_render's ray statistics
 //
 // Reference: /root/reference/Hw4/MySdlApplication.cpp (rayTraceScreen :1251-1324, rayTraceRay
 // :1184-1249, intersection code :611-823, :1084-1113).
@@ -24,242 +20,25 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/rt_api.h"
 #include "../../include/rt_diag.h"
-#include "rt_device.hpp"
 #include "rt_internal.hpp"
+#include "rt_render.hpp"
 
 using namespace rt;
 
-#ifndef RT_WAVE_TRACE
-#define RT_WAVE_TRACE 0
-#endif
-// __launch_bounds__ minimum waves per EU of the depth <= 3 render kernels.  0 (default): 6 for depth <= 2
-// (<= 80 VGPRs, no spills since the bounce loop stopped carrying the previous ray through the light loop),
-// 5 for depth 3 (<= 96 VGPRs; 6 would spill 8 B/lane).
-#ifndef RT_MINW
-#define RT_MINW 0
-#endif
-#ifndef RT_NT_STORES
-#define RT_NT_STORES 0                         // 1: non-temporal RGBA32F/RGBA8 stores (A/B)
-#endif
-#ifndef RT_WG_FAST
-#define RT_WG_FAST 64                          // workgroup of the default render kernels: 64 (8 x 8) or 128 (16 x 8)
-#endif
-#ifndef RT_MINW_CULL
-#define RT_MINW_CULL 5                         // the culling variant (>= kConeMin spheres): 87 VGPRs, no spills
-#endif
-
 namespace {
 
-constexpr int kTileW = 32;   // workgroup tile: 32 columns ...
-constexpr int kTileH = 8;    // ... x 8 rows = 256 pixels
-constexpr int kThreads = 256;
-static_assert(kThreads == kSlotStride, "one LDS colour slot column per work-item");
-
-// LDS bytes of trace()'s per-level slots for depth B: 3 doubles (+ the material id when TRANSP) per level
-// and work-item of a `wg`-thread workgroup.
-__host__ __device__ constexpr int slot_bytes(int B, bool transp, int wg = kSlotStride) {
-    return (B + 1) * (3 * 8 + (transp ? 4 : 0)) * wg;
-}
-
-struct RenderParams {
-    double eye[3];
-    double look[3];
-    double right[3];
-    double upp[3];
-    double pitch;
-    int32_t bottom_x, bottom_y;
-    int32_t width, height;
-    int32_t local_rows;                        // over all frames
-    int32_t frame_rows;                        // local rows per frame
-    int32_t frames;
-    int32_t band_height, n_ranks, rank;
-    int32_t lds_bytes;
-    int32_t np;
-    int32_t nl;
-    int32_t wg_staging;                        // 1: stage the 32 x 8 tile in LDS behind a workgroup barrier
-    float look32[3], right32[3], upp32[3], eye32[3], pitch32;   // FP32 camera for primary_cone_mask
-    float cone_slack;                          // its error bound (render_params)
-    const int32_t* tile_rows;                  // dispatch order of tile rows (nullptr: bottom to top)
-    uint32_t* row_cost;                        // calibration render: per tile row, sum of wave times (100 MHz)
-    int32_t tile_rows_n;                       // tile rows of this launch
-};
-
-constexpr int kGridY = 32768;                  // grid.y per grid.z slice
-
-// Image row (within its frame) of local row lr; local rows are frame-major (rt_rows.frames).
-__device__ __forceinline__ int global_row_of(const RenderParams& P, int lr) {
-    if (P.frames > 1) lr %= P.frame_rows;
-    if (P.n_ranks <= 1) return lr;
-    int band = lr / P.band_height, within = lr - band * P.band_height;
-    return (band * P.n_ranks + P.rank) * P.band_height + within;
-}
-
-// Copy the scene record into LDS, 16 B per work-item per step.
-__device__ __forceinline__ void stage_scene(char* dst, const DevScene* __restrict__ src, int bytes) {
-    const uint4* s = reinterpret_cast<const uint4*>(src);
-    uint4* d = reinterpret_cast<uint4*>(dst);
-    for (int k = threadIdx.x; k < (bytes >> 4); k += kThreads) d[k] = s[k];
-}
-
-// floor(clamp(c, 0, 1) * 255 + 0.5) (RGBA8 definition).  fmax/fmin (v_max/v_min_f64) clamp
-// exactly like the comparisons; NaN becomes 0 (the conversion of a NaN is 0 on the device as well).
-__device__ __forceinline__ unsigned char to_u8(double c) {
-    double v = fmin(fmax(c, 0.0), 1.0);
-    return (unsigned char)(int)floor(v * 255.0 + 0.5);
-}
+using namespace rtk;
 
 #if RT_WAVE_TRACE
-// Diagnostic build only (tools/wave_trace.py): per workgroup {start, end} shader-clock stamps and HW_ID.
-__device__ uint64_t* g_wtrace = nullptr;
+uint64_t* g_wtrace = nullptr;                  // diagnostic build only (tools/wave_trace.py)
 #endif
-
-template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false>
-__global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
-                                                             RenderParams P, float4* __restrict__ out32,
-                                                             uchar4* __restrict__ out8,
-                                                             double* __restrict__ out64,
-                                                             uint32_t* __restrict__ outrc) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x;
-#if RT_WAVE_TRACE
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#endif
-    const uint64_t t_cal = P.row_cost ? __builtin_amdgcn_s_memrealtime() : 0;
-    // LDS: [header | DevSphere[np] | DevSpherePrim[np]] (LDS = 1), the per-level colour slots of trace()
-    // (slot_bytes), then the output staging tile (12 KB, RT_WG_STAGING only).
-    // The scene record is broadcast into LDS once per workgroup; the FP32 filter images stay in global
-    // memory and are read with wave-uniform indices (scalar loads, SGPR operands).
-    int off = 0;
-    const DevScene* S = gscene;
-    if (LDS) {
-        stage_scene(smem, gscene, P.lds_bytes);
-        S = reinterpret_cast<const DevScene*>(smem);
-        off = P.lds_bytes;
-    }
-    double* slot = reinterpret_cast<double*>(smem + off) + tid;
-    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * (B + 1) * WG) + tid;
-    off += slot_bytes(B, TRANSP, WG);
-    float4* st32 = reinterpret_cast<float4*>(smem + off);                              // [8][32] 4 KB
-    double* st64 = reinterpret_cast<double*>(smem + off + 4096);                        // [8][32][3] 6 KB
-    uint32_t* strc = reinterpret_cast<uint32_t*>(smem + off + 4096 + 6144);             // [8][32] 1 KB
-    uchar4* st8 = reinterpret_cast<uchar4*>(smem + off + 4096 + 6144 + 1024);           // [8][32] 1 KB
-    if (LDS) __syncthreads();
-    const SceneView V = view_of(S, gscene, P.np, P.nl);
-    const d3 eye = ld3(P.eye);
-
-    const int wave = tid >> 6, lane = tid & 63;
-    // The 32 x 8 tile (WG = 256) is cut into 4 wave blocks of 8 x 8 pixels (square blocks keep a wave's
-    // rays coherent; 16 x 4 and 32 x 2 blocks measured no faster, and 32 x 2 slower at c5); WG = 64: one
-    // wave, one 8 x 8 tile.
-    constexpr int bw = 8, bh = 8, TW = WG / 8;
-    const int bx0 = wave * bw, by0 = 0;
-    const int cx = bx0 + (lane & 7);               // column inside the tile
-    const int cy = lane >> 3;                      // row inside the tile
-    const int tx = blockIdx.x;                      // 2-D grid: tiles_x x tiles_y
-    const int gy = (int)(blockIdx.z * kGridY + blockIdx.y);    // tile rows beyond kGridY go to grid.z
-    const int ty = P.tile_rows ? P.tile_rows[gy] : gy;
-    if ((unsigned)ty >= (unsigned)P.tile_rows_n) return;        // padding of the last grid.z slice
-    const int i = tx * TW + cx;
-    const int lr = ty * kTileH + cy;
-    const bool valid = i < P.width && lr < P.local_rows;
-
-    // Per-wave sphere culling (all lanes active here).  The block's rows must be contiguous image rows.
-    uint64_t cone = ~0ull;
-    if (P.np >= kConeMin) {
-        // Within one frame global_row_of is increasing, so jb - ja == 7 means 8 consecutive rows.
-        const int lr0 = ty * kTileH + by0, ja = global_row_of(P, lr0), jb = global_row_of(P, lr0 + bh - 1);
-        const bool one_frame = P.frames <= 1 || lr0 / P.frame_rows == (lr0 + bh - 1) / P.frame_rows;
-        const float hx = 0.5f * (float)(bw - 1), hy = 0.5f * (float)(bh - 1);
-        if (one_frame && jb - ja == bh - 1)
-            cone = primary_cone_mask(V, P.look32, P.right32, P.upp32, P.eye32, P.pitch32,
-                                     (float)(tx * TW + bx0 + P.bottom_x) + hx, (float)(ja + P.bottom_y) + hy,
-                                     sqrtf(hx * hx + hy * hy), P.cone_slack, lane);
-    }
-
-    // Every lane traces (trace() reduces over the wave): lanes outside the frame trace a clamped pixel
-    // and store nothing.
-    uint32_t seg = 0, sh = 0;
-    const int ic = i < P.width ? i : P.width - 1, lrc = lr < P.local_rows ? lr : P.local_rows - 1;
-    const int j = global_row_of(P, lrc);
-    const d3 right = ld3(P.right), upp = ld3(P.upp);
-    // Primary ray Line(camera, sp), SURVEY.md Appendix B (basis: rayTraceScreen :1270-1279).
-    const d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(ic + P.bottom_x), right)),
-                      scl(P.pitch * (double)(j + P.bottom_y), upp));
-    const d3 bdP = sub(ld3(V.S->bc), eye);                  // bounding-sphere deltaP for p0 = camera
-    d3 col;
-    if constexpr (TREE)
-        col = trace_tree<B>(V, eye, sp, &seg, &sh);
-    else
-        col = trace<B, true, TRANSP, CULL, WG>(V, eye, sp, bdP, dot(bdP, bdP), cone, &seg, &sh, slot, mslot);
-
-    if (WG != kThreads || !P.wg_staging) {
-        // Direct stores: each wave writes its 8 x 8 block as 8 row segments (128 B of RGBA32F each) and
-        // retires without waiting at a workgroup barrier for slower waves of the tile.
-        if (valid) {
-            const size_t k = (size_t)lr * P.width + i;
-#if RT_NT_STORES
-            if (out32) {
-                float* o = reinterpret_cast<float*>(out32 + k);
-                __builtin_nontemporal_store((float)col.x, o);
-                __builtin_nontemporal_store((float)col.y, o + 1);
-                __builtin_nontemporal_store((float)col.z, o + 2);
-                __builtin_nontemporal_store(1.0f, o + 3);
-            }
-#else
-            if (out32) out32[k] = make_float4((float)col.x, (float)col.y, (float)col.z, 1.0f);
-#endif
-            if (out64) { out64[3 * k] = col.x; out64[3 * k + 1] = col.y; out64[3 * k + 2] = col.z; }
-            if (outrc) outrc[k] = seg | (sh << 16);
-#if RT_NT_STORES
-            if (out8) {
-                const uint32_t px = (uint32_t)to_u8(col.x) | ((uint32_t)to_u8(col.y) << 8) |
-                                    ((uint32_t)to_u8(col.z) << 16) | (255u << 24);
-                __builtin_nontemporal_store(px, reinterpret_cast<uint32_t*>(out8 + k));
-            }
-#else
-            if (out8) out8[k] = make_uchar4(to_u8(col.x), to_u8(col.y), to_u8(col.z), 255);
-#endif
-        }
-        if (P.row_cost && tid == 0)
-            atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
-#if RT_WAVE_TRACE
-        if (g_wtrace && tid == 0) {
-            const size_t w = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-            g_wtrace[3 * w] = t_start;
-            g_wtrace[3 * w + 1] = __builtin_amdgcn_s_memrealtime();
-            g_wtrace[3 * w + 2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
-                                  ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
-        }
-#endif
-        return;
-    }
-    // Stage through LDS, then store whole tile rows.
-    const int ts = cy * kTileW + cx;
-    if (out32) st32[ts] = make_float4((float)col.x, (float)col.y, (float)col.z, 1.0f);
-    if (out64) { st64[3 * ts] = col.x; st64[3 * ts + 1] = col.y; st64[3 * ts + 2] = col.z; }
-    if (outrc) strc[ts] = seg | (sh << 16);
-    if (out8) st8[ts] = make_uchar4(to_u8(col.x), to_u8(col.y), to_u8(col.z), 255);
-    __syncthreads();
-    const int oy = tid >> 5, ox = tid & 31;
-    const int gi = tx * kTileW + ox, glr = ty * kTileH + oy;
-    if (gi < P.width && glr < P.local_rows) {
-        const size_t k = (size_t)glr * P.width + gi;
-        if (out32) out32[k] = st32[tid];
-        if (out64) {
-            out64[3 * k] = st64[3 * tid];
-            out64[3 * k + 1] = st64[3 * tid + 1];
-            out64[3 * k + 2] = st64[3 * tid + 2];
-        }
-        if (outrc) outrc[k] = strc[tid];
-        if (out8) out8[k] = st8[tid];
-    }
-    if (P.row_cost && tid == 0) atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
-}
 
 // Tile-row dispatch order from a calibration render's per-row costs: rows by decreasing cost (ties by
 // index), so the longest rows are dispatched first and the cheap ones fill the tail (longest-processing-
@@ -309,6 +88,7 @@ __global__ __launch_bounds__(kThreads) void rt_prepare_kernel(DevScene* __restri
         g->eye[0] = ex; g->eye[1] = ey; g->eye[2] = ez;
         // board plane numerator for p0 = eye, as board_hit computes it (:657)
         g->board_num = dot(ld3(g->tri[0].n), sub(ld3(g->tri[0].v0), eye));
+        g->hits_ok = hits_ok_from(g, eye);      // hit points of rays from this eye skip the cull (hits_inside)
     }
     if (k >= np) return;
     d3 dP = sub(ld3(sph[k].c), eye);
@@ -359,30 +139,6 @@ __global__ __launch_bounds__(kThreads) void rt_scene_init_kernel(DevScene* __res
     }
 }
 
-template <int B, bool TRANSP, bool TREE = false>
-__global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene* __restrict__ S,
-                                                                 const double* __restrict__ starts,
-                                                                 const double* __restrict__ ends, int n,
-                                                                 double* __restrict__ rgb,
-                                                                 uint32_t* __restrict__ rc) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    // Every lane traces (trace() reduces over the wave); lanes past n repeat ray n - 1 and store nothing.
-    const int k = blockIdx.x * kThreads + threadIdx.x, kk = k < n ? k : n - 1;
-    uint32_t seg = 0, sh = 0;
-    const SceneView V = view_of(S, S, S->n_padded, S->n_lights);
-    double* slot = reinterpret_cast<double*>(smem) + threadIdx.x;
-    int* mslot = reinterpret_cast<int*>(smem + 3 * 8 * (B + 1) * kSlotStride) + threadIdx.x;
-    d3 c;
-    if constexpr (TREE)
-        c = trace_tree<B>(V, ld3(starts + 3 * kk), ld3(ends + 3 * kk), &seg, &sh);
-    else
-        c = trace<B, false, TRANSP, false>(V, ld3(starts + 3 * kk), ld3(ends + 3 * kk), mk(0.0, 0.0, 0.0), 0.0,
-                                           ~0ull, &seg, &sh, slot, mslot);
-    if (k >= n) return;
-    if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
-    if (rc) rc[k] = seg | (sh << 16);
-}
-
 __global__ __launch_bounds__(kThreads) void rt_intersect_kernel(const DevScene* __restrict__ S,
                                                                 const double* __restrict__ starts,
                                                                 const double* __restrict__ ends, int n,
@@ -417,9 +173,18 @@ __global__ __launch_bounds__(kThreads) void rt_intersect_kernel(const DevScene* 
     hits[k] = h;
 }
 
-// One workgroup per image row; copies the row from its rank's slab (rank 0's from src0 when given: the
-// group's root does not send its own slab to itself), 16 bytes per work-item step when rows are 16-byte
-// multiples (RGBA8 rows of W % 4 == 0, every RGBA32F row), else 4.
+// Row of the gathered buffer that holds image row j: rank = band % n_ranks, local row within its slab.  Rank 0's
+// rows come from src0 when given (the group's root does not send its own slab to itself).
+__device__ __forceinline__ const uint8_t* gathered_row(const uint8_t* src, const uint8_t* src0, int j, int band_height,
+                                                       int n_ranks, int slab_rows, size_t row_bytes) {
+    const int band = j / band_height;
+    const int rank = band % n_ranks;
+    const int lr = (band / n_ranks) * band_height + (j - band * band_height);
+    return (rank == 0 && src0) ? src0 + (size_t)lr * row_bytes : src + ((size_t)rank * slab_rows + lr) * row_bytes;
+}
+
+// One workgroup per image row; copies the row from its rank's slab, 16 bytes per work-item step when rows are
+// 16-byte multiples (RGBA8 rows of W % 4 == 0, every RGBA32F row), else 4.
 template <int VEC>
 __global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* __restrict__ src,
                                                                 const uint32_t* __restrict__ src0,
@@ -428,11 +193,9 @@ __global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* 
                                                                 int slab_rows) {
     const int j = blockIdx.x;
     if (j >= height) return;
-    const int band = j / band_height;
-    const int rank = band % n_ranks;
-    const int lr = (band / n_ranks) * band_height + (j - band * band_height);
-    const uint32_t* s = (rank == 0 && src0) ? src0 + (size_t)lr * row_words
-                                            : src + ((size_t)rank * slab_rows + lr) * row_words;
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(
+        gathered_row(reinterpret_cast<const uint8_t*>(src), reinterpret_cast<const uint8_t*>(src0), j, band_height,
+                     n_ranks, slab_rows, (size_t)row_words * 4));
     uint32_t* d = dst + (size_t)j * row_words;
     if (VEC == 4) {
         const uint4* s4 = reinterpret_cast<const uint4*>(s);
@@ -443,8 +206,85 @@ __global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* 
     }
 }
 
+// Unshuffle + expand packed rows into RGBA images (the wire formats of rt_render_multi, include/rt_api.h):
+//   kUnpackGray8: GRAY8 -> RGBA8 (g, g, g, 255);  kUnpackRgb8: RGB8 -> RGBA8 (r, g, b, 255);
+//   kUnpackGray32f: GRAY32F -> RGBA32F (v, v, v, 1).
+// Exact: the render kernel writes these very bytes into the RGBA images (achromatic scenes: R = G = B bit for
+// bit).  VEC: W % 4 == 0 and 16-byte aligned buffers — 4 pixels per work-item step, 16-byte stores.
+constexpr int kUnpackGray8 = 0, kUnpackRgb8 = 1, kUnpackGray32f = 2;
+template <int MODE, bool VEC>
+__global__ __launch_bounds__(kThreads) void rt_unpack_kernel(const uint8_t* __restrict__ src,
+                                                             const uint8_t* __restrict__ src0,
+                                                             uint8_t* __restrict__ dst, int W, int height,
+                                                             int band_height, int n_ranks, int slab_rows) {
+    const int j = blockIdx.x;
+    if (j >= height) return;
+    constexpr size_t in_px = MODE == kUnpackGray8 ? 1 : MODE == kUnpackRgb8 ? 3 : 4;
+    constexpr size_t out_px = MODE == kUnpackGray32f ? 16 : 4;
+    const uint8_t* s = gathered_row(src, src0, j, band_height, n_ranks, slab_rows, (size_t)W * in_px);
+    uint8_t* d = dst + (size_t)j * W * out_px;
+    if (VEC) {
+        const int groups = W >> 2;
+        for (int q = threadIdx.x; q < groups; q += kThreads) {
+            if (MODE == kUnpackGray8) {
+                const uint32_t g = reinterpret_cast<const uint32_t*>(s)[q];
+                uint4 o;
+                o.x = (g & 0xffu) * 0x010101u | 0xff000000u;
+                o.y = ((g >> 8) & 0xffu) * 0x010101u | 0xff000000u;
+                o.z = ((g >> 16) & 0xffu) * 0x010101u | 0xff000000u;
+                o.w = (g >> 24) * 0x010101u | 0xff000000u;
+                reinterpret_cast<uint4*>(d)[q] = o;
+            } else if (MODE == kUnpackRgb8) {
+                const uint32_t* s3 = reinterpret_cast<const uint32_t*>(s) + 3 * q;
+                const uint32_t a = s3[0], b = s3[1], c = s3[2];      // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
+                uint4 o;
+                o.x = (a & 0xffffffu) | 0xff000000u;
+                o.y = (a >> 24) | ((b & 0xffffu) << 8) | 0xff000000u;
+                o.z = (b >> 16) | ((c & 0xffu) << 16) | 0xff000000u;
+                o.w = (c >> 8) | 0xff000000u;
+                reinterpret_cast<uint4*>(d)[q] = o;
+            } else {
+                const float4 v = reinterpret_cast<const float4*>(s)[q];
+                float4* o = reinterpret_cast<float4*>(d) + 4 * q;
+                o[0] = make_float4(v.x, v.x, v.x, 1.0f);
+                o[1] = make_float4(v.y, v.y, v.y, 1.0f);
+                o[2] = make_float4(v.z, v.z, v.z, 1.0f);
+                o[3] = make_float4(v.w, v.w, v.w, 1.0f);
+            }
+        }
+        return;
+    }
+    for (int x = threadIdx.x; x < W; x += kThreads) {
+        if (MODE == kUnpackGray8) {
+            const uint8_t g = s[x];
+            d[4 * x] = g; d[4 * x + 1] = g; d[4 * x + 2] = g; d[4 * x + 3] = 255;
+        } else if (MODE == kUnpackRgb8) {
+            d[4 * x] = s[3 * x]; d[4 * x + 1] = s[3 * x + 1]; d[4 * x + 2] = s[3 * x + 2]; d[4 * x + 3] = 255;
+        } else {
+            float v;
+            memcpy(&v, s + 4 * (size_t)x, 4);
+            const float4 o = make_float4(v, v, v, 1.0f);
+            memcpy(d + 16 * (size_t)x, &o, 16);
+        }
+    }
+}
+
 // rt_render's ray statistics: sums of the per-pixel counters (primary+reflect segments, shadow rays) into
 // sums[0], sums[1] (zeroed by the caller), so only 16 bytes cross PCIe instead of 4 bytes per pixel.
+// Device -> pinned host frame (rt_host_alloc memory, mapped into the device's address space): a copy kernel
+// whose 16-byte stores cross PCIe straight into the host buffer.  On the render stream it needs no cross-stream
+// hand-off, and unlike hipMemcpyAsync's SDMA path (measured on MI355X: 0.20-0.48 ms per c2 GRAY8 frame once
+// copies overlap renders, against 0.08 ms with copy kernels) it overlaps the next frame's render.
+__global__ __launch_bounds__(kThreads) void rt_copy_out_kernel(const uint8_t* __restrict__ src,
+                                                               uint8_t* __restrict__ dst, size_t n) {
+    const size_t n16 = n >> 4;
+    const size_t step = (size_t)gridDim.x * kThreads;
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    for (size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x; k < n16; k += step) d[k] = s[k];
+    if (blockIdx.x == 0 && threadIdx.x < (n & 15)) dst[(n16 << 4) + threadIdx.x] = src[(n16 << 4) + threadIdx.x];
+}
+
 __global__ __launch_bounds__(kThreads) void rt_raysum_kernel(const uint32_t* __restrict__ rc, size_t n,
                                                              unsigned long long* __restrict__ sums) {
     unsigned long long seg = 0, sh = 0;
@@ -488,59 +328,6 @@ __global__ __launch_bounds__(kThreads) void rt_probe_math_kernel(int op, const d
     o[8] = len_fast(v);
 }
 
-// ------------------------------------------------------------------------------------------------
-// Template dispatch.
-// RT_MAX_B < 7 (experiment builds only, tools/variants.sh): deeper kernels are not instantiated.
-#ifndef RT_MAX_B
-#define RT_MAX_B 7
-#endif
-// MINW = 0: the depth-dependent default of RT_MINW (6 for depth <= 2, else 5).
-template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG, bool TREE>
-hipError_t launch_render_one(dim3 grid, size_t lds, hipStream_t st, const DevScene* s, const RenderParams& P,
-                             float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
-    constexpr int MW = MINW != 0 ? MINW : (B <= 2 ? 6 : 5);
-    if constexpr (B > RT_MAX_B) {
-        return hipErrorInvalidValue;
-    } else {
-        if (lds > 65536) {
-            hipError_t e = hipFuncSetAttribute((const void*)rt_render_kernel<B, LDS, MW, TRANSP, CULL, WG, TREE>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-        }
-        hipLaunchKernelGGL((rt_render_kernel<B, LDS, MW, TRANSP, CULL, WG, TREE>), grid, dim3(WG), lds, st, s, P, o32, o8,
-                           o64, orc);
-        return hipGetLastError();
-    }
-}
-
-template <int LDS, int MINW, bool TRANSP, bool CULL = false, int WG = kThreads, bool TREE = false>
-hipError_t launch_render_lds(int depth, dim3 grid, size_t lds, hipStream_t st, const DevScene* s,
-                             const RenderParams& P, float4* o32, uchar4* o8, double* o64, uint32_t* orc) {
-#define RT_CASE(b) \
-    case b: return launch_render_one<b, LDS, MINW, TRANSP, CULL, WG, TREE>(grid, lds, st, s, P, o32, o8, o64, orc);
-    switch (depth) {
-        RT_CASE(0) RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7)
-        default: return hipErrorInvalidValue;
-    }
-#undef RT_CASE
-}
-
-template <bool TRANSP, bool TREE = false>
-hipError_t launch_trace_rays(int depth, dim3 grid, hipStream_t st, const DevScene* s, const double* a,
-                             const double* b, int n, double* rgb, uint32_t* rc) {
-#define RT_CASE(k)                                                                                      \
-    case k:                                                                                             \
-        hipLaunchKernelGGL((rt_trace_rays_kernel<k, TRANSP, TREE>), grid, dim3(kThreads), TREE ? 0 : slot_bytes(k, TRANSP), st, s, \
-                           a, b, n, rgb, rc);                                                           \
-        break;
-    switch (depth) {
-        RT_CASE(0) RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7)
-        default: return hipErrorInvalidValue;
-    }
-#undef RT_CASE
-    return hipGetLastError();
-}
-
 }  // namespace
 
 // ================================================================================================
@@ -557,6 +344,7 @@ struct rt_ctx {
     bool scene_set = false;
     bool transparent = false;                  // some material is transparent: TRANSP kernel variants
     bool tree = false;                         // some material transmits and reflects: TREE kernel variants
+    bool achromatic = false;                   // R = G = B everywhere (rt_scene_achromatic): GRAY formats allowed
     bool eye_valid = false;                    // the device *Prim arrays hold data for `eye`
     bool ever_captured = false;                // a render was captured into a hipGraph: replays may rewrite
                                                // the per-eye data, so every later render re-prepares it
@@ -566,6 +354,11 @@ struct rt_ctx {
                                                // than no bound: tools/ab.py); RT_MIN_WAVES=0 disables
     int use_lds = 0;                           // RT_SCENE_IN_LDS=1: header + exact records in LDS (A/B: tools/ab.py)
     int wg_staging = 0;                        // RT_WG_STAGING=1: LDS-staged 32-pixel row stores (A/B)
+    // RT_COPY_MODE (A/B): 1 (default) host copies queued behind the render on the render stream, 0 on the copy
+    // stream behind a cross-stream event.  Measured at c2 GRAY8 with copy kernels: synchronous 0.089 vs 0.100 ms
+    // per call, pipelined 0.079 either way (tools/packed_probe.py).
+    int copy_mode = 1;
+    int copy_kernel = 1;                       // RT_COPY_KERNEL=0: hipMemcpyAsync for rt_host_alloc memory too (A/B)
     // Adaptive tile-row order (rt_order_kernel): the first render of a new (scene, camera, size, rows,
     // depth, outputs) view uses the identity order; the second render of the same view is a calibration
     // render that also times its tile rows; later renders dispatch the rows by decreasing time.  A render
@@ -586,9 +379,19 @@ struct rt_ctx {
     int order_mode = 0;
     uint64_t scene_gen = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    // rt_render's device buffers (grow-only, reused across calls): rgba32f, rgba8, rgb64f, raycount, sums
-    void* d_out[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    size_t out_cap[5] = {0, 0, 0, 0, 0};
+    // The host-buffer calls (rt_render, rt_render_packed, rt_render_packed_async) run on the context's own
+    // streams: renders on `rs` (blocking w.r.t. the null stream, like the null-stream renders it replaced), the
+    // device-to-host copies on `cs`, so an asynchronous frame's copy overlaps the next frame's render.
+    hipStream_t rs = nullptr, cs = nullptr;
+    hipEvent_t rendered[2] = {nullptr, nullptr};   // slot b's packed frame is in its device buffer
+    hipEvent_t copied[2] = {nullptr, nullptr};     // slot b's packed frame is in its host buffer
+    bool copied_rec[2] = {false, false};
+    uint64_t ticket = 0;                       // rt_render_packed_async frames queued so far
+    // rt_render's device buffers (grow-only, reused across calls): rgba32f, rgba8, rgb64f, raycount, sums,
+    // packed slot 0, packed slot 1
+    static constexpr int kBufs = 7;
+    void* d_out[kBufs] = {};
+    size_t out_cap[kBufs] = {};
 };
 
 #define RT_HIP(call)                                                                                  \
@@ -599,7 +402,8 @@ struct rt_ctx {
 
 #if RT_WAVE_TRACE
 extern "C" int rt_debug_wave_trace(void* dev_buf) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace), &dev_buf, sizeof(dev_buf)) == hipSuccess ? RT_OK : RT_EHIP;
+    g_wtrace = reinterpret_cast<uint64_t*>(dev_buf);
+    return RT_OK;
 }
 #endif
 
@@ -612,6 +416,28 @@ extern "C" int rt_device_count(int* count) {
         return rt_fail(RT_EHIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
     }
     *count = n;
+    return RT_OK;
+}
+
+extern "C" int rt_ctx_destroy(rt_ctx* c) {
+    if (!c) return RT_OK;
+    (void)hipSetDevice(c->device);
+    if (c->rs) (void)hipStreamSynchronize(c->rs);
+    if (c->cs) (void)hipStreamSynchronize(c->cs);
+    if (c->d_scene) (void)hipFree(c->d_scene);
+    if (c->d_tile_rows) (void)hipFree(c->d_tile_rows);
+    if (c->d_row_cost) (void)hipFree(c->d_row_cost);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (int b = 0; b < 2; ++b) {
+        if (c->rendered[b]) (void)hipEventDestroy(c->rendered[b]);
+        if (c->copied[b]) (void)hipEventDestroy(c->copied[b]);
+    }
+    if (c->rs) (void)hipStreamDestroy(c->rs);
+    if (c->cs) (void)hipStreamDestroy(c->cs);
+    for (void* p : c->d_out)
+        if (p) (void)hipFree(p);
+    delete c;
     return RT_OK;
 }
 
@@ -629,19 +455,24 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_MIN_WAVES")) c->min_waves = atoi(e);
     if (const char* e = getenv("RT_WG_STAGING")) c->wg_staging = atoi(e) != 0;
     if (const char* e = getenv("RT_TILE_ORDER")) c->order_mode = atoi(e) == 1 ? 1 : 0;   // 1: bottom-to-top (A/B)
+    if (const char* e = getenv("RT_COPY_MODE")) c->copy_mode = atoi(e) == 0 ? 0 : 1;
+    if (const char* e = getenv("RT_COPY_KERNEL")) c->copy_kernel = atoi(e) != 0;
     if (hipMalloc(&c->d_tile_rows, sizeof(int32_t) * kOrderMax) != hipSuccess ||
         hipMalloc(&c->d_row_cost, sizeof(uint32_t) * kOrderMax) != hipSuccess) {
         rt_ctx_destroy(c);
         return rt_fail(RT_ENOMEM, "rt_ctx_create: hipMalloc of the tile-row order failed");
     }
     c->n_tile_rows = kOrderMax;
-    if (hipMemset(c->d_tile_rows, 0, sizeof(int32_t) * kOrderMax) != hipSuccess) {
+    bool ok = hipMemset(c->d_tile_rows, 0, sizeof(int32_t) * kOrderMax) == hipSuccess &&
+              hipEventCreate(&c->ev0) == hipSuccess && hipEventCreate(&c->ev1) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->rs, hipStreamDefault) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking) == hipSuccess;
+    for (int b = 0; b < 2 && ok; ++b)
+        ok = hipEventCreateWithFlags(&c->rendered[b], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->copied[b], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
         rt_ctx_destroy(c);
-        return rt_fail(RT_EHIP, "rt_ctx_create: hipMemset of the tile-row order failed");
-    }
-    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
-        delete c;
-        return rt_fail(RT_EHIP, "rt_ctx_create: hipEventCreate failed");
+        return rt_fail(RT_EHIP, "rt_ctx_create: stream/event creation failed");
     }
     *out = c;
     return RT_OK;
@@ -649,19 +480,7 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
 
 int rt_ctx_device(const rt_ctx* c) { return c ? c->device : -1; }
 
-extern "C" int rt_ctx_destroy(rt_ctx* c) {
-    if (!c) return RT_OK;
-    (void)hipSetDevice(c->device);
-    if (c->d_scene) (void)hipFree(c->d_scene);
-    if (c->d_tile_rows) (void)hipFree(c->d_tile_rows);
-    if (c->d_row_cost) (void)hipFree(c->d_row_cost);
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
-    for (void* p : c->d_out)
-        if (p) (void)hipFree(p);
-    delete c;
-    return RT_OK;
-}
+int rt_ctx_achromatic(const rt_ctx* c) { return c && c->scene_set && c->achromatic ? 1 : 0; }
 
 extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     if (!c) return rt_fail(RT_EINVAL, "rt_set_scene: null context");
@@ -671,6 +490,9 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     // An unchanged scene (same flattened record, byte for byte) keeps the device copy, the per-eye data
     // and the tile-row order: rt_render calls this every frame.
     if (c->scene_set && blob == c->blob) return RT_OK;
+    int achromatic = 0;
+    rc = rt_scene_achromatic(scene, &achromatic);
+    if (rc) return rc;
     RT_HIP(hipSetDevice(c->device));
     // Renders still in flight on any stream of this device read d_scene: wait for them before it changes.
     RT_HIP(hipDeviceSynchronize());
@@ -695,6 +517,7 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     c->n_lights = h->n_lights;
     c->transparent = h->transparent != 0 || h->n_meshes > 0;   // FULL kernel variants
     c->tree = h->tree != 0;
+    c->achromatic = achromatic != 0;
     c->eye_valid = false;
     c->scene_set = true;
     c->blob.swap(blob);
@@ -737,6 +560,9 @@ static int render_params(const rt_ctx* c, const rt_camera* cam, int W, int H, in
     P->np = c->n_padded;
     P->nl = c->n_lights;
     P->wg_staging = c->wg_staging;
+#if RT_WAVE_TRACE
+    P->wtrace = g_wtrace;
+#endif
     // FP32 camera for the per-wave cone culling, and the bound on its error as a chord distance: every
     // FP32 coordinate is below M in magnitude and carries < 16 roundings, and |sp - eye| >= |look - eye|
     // (right, up' are orthogonal to look - eye), so direction errors are < 64 eps32 M / |look - eye|.
@@ -756,18 +582,44 @@ static int render_params(const rt_ctx* c, const rt_camera* cam, int W, int H, in
     return RT_OK;
 }
 
-extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int depth, const rt_rows* rows,
-                             float* rgba32f, uint8_t* rgba8, double* rgb64f, uint32_t* raycount, void* stream) {
+static bool float_format(int f) { return f == RT_PIXEL_RGBA32F || f == RT_PIXEL_GRAY32F; }
+static bool byte_format(int f) { return f == RT_PIXEL_RGBA8 || f == RT_PIXEL_RGB8 || f == RT_PIXEL_GRAY8; }
+
+extern "C" int rt_pixel_bytes(int format, int* bytes) {
+    if (!bytes) return rt_fail(RT_EINVAL, "rt_pixel_bytes: null pointer");
+    switch (format) {
+        case RT_PIXEL_RGBA32F: *bytes = 16; return RT_OK;
+        case RT_PIXEL_GRAY32F: *bytes = 4; return RT_OK;
+        case RT_PIXEL_RGBA8: *bytes = 4; return RT_OK;
+        case RT_PIXEL_RGB8: *bytes = 3; return RT_OK;
+        case RT_PIXEL_GRAY8: *bytes = 1; return RT_OK;
+        default: *bytes = 0; return rt_fail(RT_EINVAL, "rt_pixel_bytes: unknown pixel format");
+    }
+}
+
+// The device render behind rt_render_dev / rt_render_dev_packed: the float image (fmt_f) and the byte image
+// (fmt_8) in their formats, the FP64 colour and the ray counters, each nullable.
+static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int depth, const rt_rows* rows,
+                           int fmt_f, void* pf, int fmt_8, void* p8, double* rgb64f, uint32_t* raycount,
+                           void* stream) {
     RenderParams P;
     int rc = render_params(c, cam, W, H, depth, rows, &P);
     if (rc) return rc;
+    if ((pf && !float_format(fmt_f)) || (p8 && !byte_format(fmt_8)))
+        return rt_fail(RT_EINVAL, "render: bad pixel format for the float / byte image");
+    if (((pf && fmt_f == RT_PIXEL_GRAY32F) || (p8 && fmt_8 == RT_PIXEL_GRAY8)) && !c->achromatic)
+        return rt_fail(RT_EINVAL, "render: GRAY pixel formats need an achromatic scene (rt_scene_achromatic)");
+    P.fmt_f = fmt_f == RT_PIXEL_GRAY32F ? kFmtF_GRAY : kFmtF_RGBA;
+    P.fmt_8 = fmt_8 == RT_PIXEL_GRAY8 ? kFmt8_GRAY : fmt_8 == RT_PIXEL_RGB8 ? kFmt8_RGB : kFmt8_RGBA;
+    const bool packed = (pf && P.fmt_f != kFmtF_RGBA) || (p8 && P.fmt_8 != kFmt8_RGBA);
+    if (packed) P.wg_staging = 0;                   // the LDS-staged stores (A/B variant) write RGBA only
     if (P.local_rows == 0) return RT_OK;
     RT_HIP(hipSetDevice(c->device));
     // One-wave workgroups (8 x 8 tiles) by default: measured faster than 256-thread workgroups (32 x 8
     // tiles) at every config (c2 -1%, c3 -3%, c5 -12%: a finished wave's slot is refilled without
     // waiting for three siblings).  The A/B variants that share a workgroup-wide LDS copy (scene in LDS,
     // staged row stores) keep 256 threads.
-    const bool big = c->use_lds || c->wg_staging;
+    const bool big = !packed && (c->use_lds || c->wg_staging);    // packed formats: one-wave variants only
     const int tw = big ? kTileW : RT_WG_FAST / 8;
     const int tiles_x = (W + tw - 1) / tw;
     const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
@@ -785,9 +637,10 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
         // Key of the frame's work: camera, size, outputs, row plan, depth and scene generation.
         unsigned char* kp = key.data();                 // fixed size: no host allocation per render
         memcpy(kp, cam, sizeof(rt_camera)); kp += sizeof(rt_camera);
-        // which outputs are written changes the rows' relative cost (an RGB64F parity render writes
-        // 24 B per pixel): each output set gets its own calibration
-        const int outs = (rgba32f ? 1 : 0) | (rgba8 ? 2 : 0) | (rgb64f ? 4 : 0) | (raycount ? 8 : 0);
+        // which outputs are written (and in which format) changes the rows' relative cost (an RGB64F parity
+        // render writes 24 B per pixel): each output set gets its own calibration
+        const int outs = (pf ? 1 : 0) | (p8 ? 2 : 0) | (rgb64f ? 4 : 0) | (raycount ? 8 : 0) | (P.fmt_f << 4) |
+                         (P.fmt_8 << 6);
         const int ints[6] = {W, H, depth, tiles_x, tiles_y, outs};
         memcpy(kp, ints, sizeof(ints)); kp += sizeof(ints);
         if (rows) memcpy(kp, rows, sizeof(rt_rows));
@@ -816,9 +669,7 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
             c->seen_valid = true;
         }
     }
-    dim3 grid((unsigned)tiles_x, (unsigned)std::min(tiles_y, kGridY), (unsigned)((tiles_y + kGridY - 1) / kGridY));
-    const size_t lds64 = slot_bytes(depth, c->transparent, 64);
-    const size_t lds256 = (c->wg_staging ? 4096 + 6144 + 1024 + 1024 : 0) + slot_bytes(depth, c->transparent);
+    const dim3 grid((unsigned)tiles_x, (unsigned)std::min(tiles_y, kGridY), (unsigned)((tiles_y + kGridY - 1) / kGridY));
     hipError_t e;
     // Primary-ray sphere data for this eye (stream-ordered; only when the eye changes, or always once graphs
     // that carry their own prepare launch exist).
@@ -832,26 +683,48 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
         memcpy(c->eye, cam->eye, sizeof(c->eye));
         c->eye_valid = true;
     }
+    RenderLaunch L;
+    L.grid = grid;
+    L.stream = st;
+    L.scene = c->d_scene;
+    L.P = P;
+    L.o32 = pf;
+    L.o8 = p8;
+    L.o64 = rgb64f;
+    L.orc = raycount;
     const bool cull = c->n_padded >= kConeMin, mw5 = c->min_waves >= 5 && depth <= 3;
-    float4* o32 = reinterpret_cast<float4*>(rgba32f);
-    uchar4* o8 = reinterpret_cast<uchar4*>(rgba8);
-    if (c->tree)
-        e = launch_render_lds<0, 1, true, false, 64, true>(depth, grid, 0, st, c->d_scene, P, o32, o8, rgb64f, raycount);
-    else if (c->transparent)
-        e = launch_render_lds<0, 1, true, false, 64>(depth, grid, lds64, st, c->d_scene, P, o32, o8, rgb64f, raycount);
-    else if (c->use_lds)
-        e = launch_render_lds<1, 1, false, false, kThreads>(depth, grid, c->lds_bytes + lds256, st, c->d_scene, P,
-                                                             o32, o8, rgb64f, raycount);
-    else if (c->wg_staging)
-        e = (mw5 ? launch_render_lds<0, RT_MINW, false, false, kThreads> : launch_render_lds<0, 1, false, false, kThreads>)(
-                depth, grid, lds256, st, c->d_scene, P, o32, o8, rgb64f, raycount);
-    else {
+    if (c->tree) {
+        L.variant = kVarTree;
+        L.lds = 0;
+    } else if (c->transparent) {
+        L.variant = kVarTransp;
+        L.lds = slot_bytes(depth, true, 64);
+    } else if (c->use_lds) {
+        L.variant = kVarLds;
+        L.lds = c->lds_bytes + slot_bytes(depth, false);
+    } else if (c->wg_staging) {
+        L.variant = mw5 ? kVarStaging : kVarStagingAnyW;
+        L.lds = 4096 + 6144 + 1024 + 1024 + slot_bytes(depth, false);
+    } else {
         // >= kConeMin spheres: the wave-culling variant (secondary and shadow rays, rt_device.hpp CULL).
-        auto launch = cull ? (mw5 ? launch_render_lds<0, RT_MINW_CULL, false, true, RT_WG_FAST>
-                                  : launch_render_lds<0, 1, false, true, RT_WG_FAST>)
-                           : (mw5 ? launch_render_lds<0, RT_MINW, false, false, RT_WG_FAST>
-                                  : launch_render_lds<0, 1, false, false, RT_WG_FAST>);
-        e = launch(depth, grid, slot_bytes(depth, false, RT_WG_FAST), st, c->d_scene, P, o32, o8, rgb64f, raycount);
+        L.variant = cull ? (mw5 ? kVarCull : kVarCullAnyW) : (mw5 ? kVarFast : kVarFastAnyW);
+        L.lds = slot_bytes(depth, false, RT_WG_FAST);
+    }
+    if (packed) {                                       // the instances with runtime pixel-format stores
+        if (c->tree) L.variant = kVarTreePacked;
+        else if (c->transparent) L.variant = kVarTranspPacked;
+        else L.variant = cull ? kVarCullPacked : kVarFastPacked;
+        if (!c->tree && !c->transparent) L.lds = slot_bytes(depth, false, RT_WG_FAST);
+    }
+    switch (depth) {
+        case 0: e = launch_render<0>(L); break;
+        case 1: e = launch_render<1>(L); break;
+        case 2: e = launch_render<2>(L); break;
+        case 3: e = launch_render<3>(L); break;
+        case 4: e = launch_render<4>(L); break;
+        case 5: e = launch_render<5>(L); break;
+        case 6: e = launch_render<6>(L); break;
+        default: e = launch_render<7>(L); break;
     }
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_kernel launch: ") + hipGetErrorString(e));
     if (calibrate) {
@@ -865,9 +738,25 @@ extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int 
     return RT_OK;
 }
 
+extern "C" int rt_render_dev(rt_ctx* c, const rt_camera* cam, int W, int H, int depth, const rt_rows* rows,
+                             float* rgba32f, uint8_t* rgba8, double* rgb64f, uint32_t* raycount, void* stream) {
+    return render_dev_impl(c, cam, W, H, depth, rows, RT_PIXEL_RGBA32F, rgba32f, RT_PIXEL_RGBA8, rgba8, rgb64f,
+                           raycount, stream);
+}
+
+extern "C" int rt_render_dev_packed(rt_ctx* c, const rt_camera* cam, int W, int H, int depth, const rt_rows* rows,
+                                    int float_format, void* float_pixels, int byte_format, void* byte_pixels,
+                                    void* stream) {
+    return render_dev_impl(c, cam, W, H, depth, rows, float_format, float_pixels, byte_format, byte_pixels, nullptr,
+                           nullptr, stream);
+}
+
 // Grow-only device buffer k of the context (rt_render's outputs).
 static int ctx_buffer(rt_ctx* c, int k, size_t bytes, void** out) {
     if (bytes > c->out_cap[k]) {
+        // the buffer may still be read by a copy (or written by a render) queued on the context's streams
+        RT_HIP(hipStreamSynchronize(c->rs));
+        RT_HIP(hipStreamSynchronize(c->cs));
         if (c->d_out[k]) (void)hipFree(c->d_out[k]);
         c->d_out[k] = nullptr;
         c->out_cap[k] = 0;
@@ -876,6 +765,56 @@ static int ctx_buffer(rt_ctx* c, int k, size_t bytes, void** out) {
         c->out_cap[k] = bytes;
     }
     *out = c->d_out[k];
+    return RT_OK;
+}
+
+// Ray statistics of a render with per-pixel counters d_rc (npx pixels) into *stats (the stream must be done).
+static int read_stats(rt_ctx* c, size_t npx, const unsigned long long* d_sums, rt_stats* stats) {
+    unsigned long long sums[2] = {0, 0};
+    if (npx) RT_HIP(hipMemcpy(sums, d_sums, sizeof(sums), hipMemcpyDeviceToHost));
+    stats->primary_rays = npx;
+    stats->reflect_rays = sums[0] - npx;
+    stats->shadow_rays = sums[1];
+    float ms = 0.f;
+    if (npx) RT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    stats->kernel_ms = ms;
+    return RT_OK;
+}
+
+// rt_host_alloc's pinned allocations (host base -> size, device mapping): host frames that land in one are
+// copied by rt_copy_out_kernel, everything else by hipMemcpyAsync (pageable memory is staged by HIP).
+static std::mutex g_pinned_mu;
+static std::map<uintptr_t, std::pair<size_t, uintptr_t>> g_pinned;
+
+static void* pinned_device_ptr(const void* host, size_t bytes) {
+    std::lock_guard<std::mutex> lk(g_pinned_mu);
+    const uintptr_t h = (uintptr_t)host;
+    auto it = g_pinned.upper_bound(h);
+    if (it == g_pinned.begin()) return nullptr;
+    --it;
+    if (h + bytes > it->first + it->second.first) return nullptr;
+    return (void*)(it->second.second + (h - it->first));
+}
+
+static int copy_to_host(rt_ctx* c, void* host, const void* dev, size_t bytes, hipStream_t st) {
+    if (!bytes) return RT_OK;
+    void* dmap = pinned_device_ptr(host, bytes);
+    if (dmap && c->copy_kernel && ((uintptr_t)dmap | (uintptr_t)dev) % 16 == 0) {
+        const unsigned blocks = (unsigned)std::min<size_t>((bytes / 16 + kThreads - 1) / kThreads + 1, 1024);
+        hipLaunchKernelGGL(rt_copy_out_kernel, dim3(blocks), dim3(kThreads), 0, st, (const uint8_t*)dev,
+                           (uint8_t*)dmap, bytes);
+        RT_HIP(hipGetLastError());
+        return RT_OK;
+    }
+    RT_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
+    return RT_OK;
+}
+
+static int queue_raysum(rt_ctx* c, size_t npx, uint32_t* d_rc, unsigned long long* d_sums) {
+    RT_HIP(hipMemsetAsync(d_sums, 0, 2 * sizeof(unsigned long long), c->rs));
+    hipLaunchKernelGGL(rt_raysum_kernel, dim3((unsigned)std::min<size_t>((npx + kThreads - 1) / kThreads, 1024)),
+                       dim3(kThreads), 0, c->rs, (const uint32_t*)d_rc, npx, d_sums);
+    RT_HIP(hipGetLastError());
     return RT_OK;
 }
 
@@ -894,36 +833,125 @@ extern "C" int rt_render(rt_ctx* c, const rt_scene* scene, const rt_camera* cam,
     const bool want[5] = {rgba32f != nullptr, rgba8 != nullptr, rgb64f != nullptr, stats != nullptr, stats != nullptr};
     for (int k = 0; k < 5; ++k)
         if (want[k] && npx > 0 && (rc = ctx_buffer(c, k, bytes[k], &d[k])) != RT_OK) return rc;
-    hipError_t e = hipEventRecord(c->ev0, nullptr);
-    if (e == hipSuccess) {
-        rc = rt_render_dev(c, cam, W, H, depth, rows, (float*)d[0], (uint8_t*)d[1], (double*)d[2], (uint32_t*)d[3],
-                           nullptr);
-        if (rc) return rc;
-        e = hipEventRecord(c->ev1, nullptr);
+    RT_HIP(hipEventRecord(c->ev0, c->rs));
+    rc = rt_render_dev(c, cam, W, H, depth, rows, (float*)d[0], (uint8_t*)d[1], (double*)d[2], (uint32_t*)d[3], c->rs);
+    if (rc) return rc;
+    RT_HIP(hipEventRecord(c->ev1, c->rs));
+    if (stats && npx > 0 && (rc = queue_raysum(c, npx, (uint32_t*)d[3], (unsigned long long*)d[4]))) return rc;
+    // asynchronous copies on the render stream (rt_host_alloc memory: a copy kernel; other memory: hipMemcpyAsync),
+    // one synchronisation of that stream (not of the device: other streams' work is not waited for)
+    void* host[3] = {rgba32f, rgba8, rgb64f};
+    for (int k = 0; k < 3; ++k)
+        if (host[k] && npx && (rc = copy_to_host(c, host[k], d[k], bytes[k], c->rs))) return rc;
+    RT_HIP(hipStreamSynchronize(c->rs));
+    if (stats) return read_stats(c, npx, (const unsigned long long*)d[4], stats);
+    return RT_OK;
+}
+
+// rt_render_packed / rt_render_packed_async: one image in `format`, copied to host memory.
+static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera* cam, int W, int H, int depth,
+                               int format, void* host, int slot, bool with_stats, size_t* npx_out, void** sums) {
+    if (!c) return rt_fail(RT_EINVAL, "rt_render_packed: null context");
+    if (!host) return rt_fail(RT_EINVAL, "rt_render_packed: null host buffer");
+    int pb = 0;
+    int rc = rt_pixel_bytes(format, &pb);
+    if (rc) return rc;
+    rc = rt_set_scene(c, scene);
+    if (rc) return rc;
+    RenderParams P;
+    rc = render_params(c, cam, W, H, depth, nullptr, &P);
+    if (rc) return rc;
+    RT_HIP(hipSetDevice(c->device));
+    const size_t npx = (size_t)W * H;
+    *npx_out = npx;
+    void* px = nullptr;
+    void* rcb = nullptr;
+    if ((rc = ctx_buffer(c, 5 + slot, npx * pb, &px))) return rc;
+    if (with_stats && ((rc = ctx_buffer(c, 3, npx * 4, &rcb)) || (rc = ctx_buffer(c, 4, 16, sums)))) return rc;
+    const hipStream_t cs = c->copy_mode == 1 ? c->rs : c->cs;
+    // the slot's device buffer is free once its previous frame's copy has left (stream-ordered on the GPU)
+    if (c->copied_rec[slot] && cs != c->rs) RT_HIP(hipStreamWaitEvent(c->rs, c->copied[slot], 0));
+    if (with_stats) RT_HIP(hipEventRecord(c->ev0, c->rs));
+    const bool f = float_format(format);
+    rc = render_dev_impl(c, cam, W, H, depth, nullptr, f ? format : RT_PIXEL_RGBA32F, f ? px : nullptr,
+                         f ? RT_PIXEL_RGBA8 : format, f ? nullptr : px, nullptr, (uint32_t*)rcb, c->rs);
+    if (rc) return rc;
+    if (with_stats) RT_HIP(hipEventRecord(c->ev1, c->rs));
+    if (with_stats && (rc = queue_raysum(c, npx, (uint32_t*)rcb, (unsigned long long*)*sums))) return rc;
+    if (cs != c->rs) {
+        // the copy runs on the copy stream, so it overlaps the next frame's render
+        RT_HIP(hipEventRecord(c->rendered[slot], c->rs));
+        RT_HIP(hipStreamWaitEvent(cs, c->rendered[slot], 0));
     }
-    if (e == hipSuccess && stats && npx > 0) {
-        e = hipMemsetAsync(d[4], 0, bytes[4], nullptr);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(rt_raysum_kernel, dim3((unsigned)std::min<size_t>((npx + kThreads - 1) / kThreads, 1024)),
-                               dim3(kThreads), 0, nullptr, (const uint32_t*)d[3], npx, (unsigned long long*)d[4]);
-            e = hipGetLastError();
-        }
+    if ((rc = copy_to_host(c, host, px, npx * pb, cs))) return rc;
+    RT_HIP(hipEventRecord(c->copied[slot], cs));
+    c->copied_rec[slot] = true;
+    return RT_OK;
+}
+
+extern "C" int rt_render_packed(rt_ctx* c, const rt_scene* scene, const rt_camera* cam, int W, int H, int depth,
+                                int format, void* host_pixels, rt_stats* stats) {
+    size_t npx = 0;
+    void* sums = nullptr;
+    if (c) c->ticket++;
+    int rc = render_packed_queue(c, scene, cam, W, H, depth, format, host_pixels, c ? (int)(c->ticket & 1) : 0,
+                                 stats != nullptr, &npx, &sums);
+    if (rc) return rc;
+    RT_HIP(hipEventSynchronize(c->copied[c->ticket & 1]));
+    if (stats) {
+        RT_HIP(hipStreamSynchronize(c->rs));
+        return read_stats(c, npx, (const unsigned long long*)sums, stats);
     }
-    if (e == hipSuccess && rgba32f && npx) e = hipMemcpy(rgba32f, d[0], bytes[0], hipMemcpyDeviceToHost);
-    if (e == hipSuccess && rgba8 && npx) e = hipMemcpy(rgba8, d[1], bytes[1], hipMemcpyDeviceToHost);
-    if (e == hipSuccess && rgb64f && npx) e = hipMemcpy(rgb64f, d[2], bytes[2], hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e == hipSuccess && stats) {
-        unsigned long long sums[2] = {0, 0};
-        if (npx) e = hipMemcpy(sums, d[4], sizeof(sums), hipMemcpyDeviceToHost);
-        stats->primary_rays = npx;
-        stats->reflect_rays = sums[0] - npx;
-        stats->shadow_rays = sums[1];
-        float ms = 0.f;
-        if (e == hipSuccess && npx) e = hipEventElapsedTime(&ms, c->ev0, c->ev1);
-        stats->kernel_ms = ms;
+    return RT_OK;
+}
+
+extern "C" int rt_render_packed_async(rt_ctx* c, const rt_scene* scene, const rt_camera* cam, int W, int H,
+                                      int depth, int format, void* host_pixels, uint64_t* ticket) {
+    size_t npx = 0;
+    void* sums = nullptr;
+    if (!c) return rt_fail(RT_EINVAL, "rt_render_packed_async: null context");
+    const uint64_t t = c->ticket + 1;
+    int rc = render_packed_queue(c, scene, cam, W, H, depth, format, host_pixels, (int)(t & 1), false, &npx, &sums);
+    if (rc) return rc;
+    c->ticket = t;
+    if (ticket) *ticket = t;
+    return RT_OK;
+}
+
+extern "C" int rt_ctx_wait(rt_ctx* c, uint64_t ticket) {
+    if (!c) return rt_fail(RT_EINVAL, "rt_ctx_wait: null context");
+    if (ticket > c->ticket) return rt_fail(RT_EINVAL, "rt_ctx_wait: ticket not issued");
+    RT_HIP(hipSetDevice(c->device));
+    if (ticket == 0) {                                  // everything queued on the context's streams
+        RT_HIP(hipStreamSynchronize(c->rs));
+        RT_HIP(hipStreamSynchronize(c->cs));
+        return RT_OK;
     }
-    if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render: ") + hipGetErrorString(e));
+    // slot (ticket & 1) holds this frame's copy or a later one's (which the GPU orders after it)
+    if (c->copied_rec[ticket & 1]) RT_HIP(hipEventSynchronize(c->copied[ticket & 1]));
+    return RT_OK;
+}
+
+extern "C" int rt_host_alloc(size_t bytes, void** out) {
+    if (!out || bytes == 0) return rt_fail(RT_EINVAL, "rt_host_alloc: bad arguments");
+    *out = nullptr;
+    RT_HIP(hipHostMalloc(out, bytes, hipHostMallocDefault));
+    void* dmap = nullptr;
+    if (hipHostGetDevicePointer(&dmap, *out, 0) != hipSuccess || !dmap) dmap = nullptr;
+    if (dmap) {                                         // host frames in it are copied by rt_copy_out_kernel
+        std::lock_guard<std::mutex> lk(g_pinned_mu);
+        g_pinned[(uintptr_t)*out] = {bytes, (uintptr_t)dmap};
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_host_free(void* p) {
+    if (!p) return RT_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_pinned_mu);
+        g_pinned.erase((uintptr_t)p);
+    }
+    RT_HIP(hipHostFree(p));
     return RT_OK;
 }
 
@@ -934,10 +962,20 @@ extern "C" int rt_trace_rays_dev(rt_ctx* c, const double* starts, const double* 
     if (depth < 0 || depth > RT_MAX_DEPTH) return rt_fail(RT_EINVAL, "rt_trace_rays_dev: depth out of range");
     if (n == 0) return RT_OK;
     RT_HIP(hipSetDevice(c->device));
-    dim3 grid((unsigned)((n + kThreads - 1) / kThreads));
-    hipError_t e = (c->tree ? launch_trace_rays<true, true>
-                    : c->transparent ? launch_trace_rays<true> : launch_trace_rays<false>)(
-        depth, grid, (hipStream_t)stream, c->d_scene, starts, ends, n, rgb64f, raycount);
+    const dim3 grid((unsigned)((n + kThreads - 1) / kThreads));
+    const int v = c->tree ? 2 : c->transparent ? 1 : 0;
+    const hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    switch (depth) {
+        case 0: e = launch_trace_rays<0>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
+        case 1: e = launch_trace_rays<1>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
+        case 2: e = launch_trace_rays<2>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
+        case 3: e = launch_trace_rays<3>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
+        case 4: e = launch_trace_rays<4>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
+        case 5: e = launch_trace_rays<5>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
+        case 6: e = launch_trace_rays<6>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
+        default: e = launch_trace_rays<7>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
+    }
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_trace_rays_kernel: ") + hipGetErrorString(e));
     return RT_OK;
 }
@@ -956,20 +994,27 @@ extern "C" int rt_intersect_dev(rt_ctx* c, const double* starts, const double* e
     return RT_OK;
 }
 
-int rt_unshuffle_dev_ex(const void* gathered, const void* rank0_slab, void* image, int W, int H, int elem_bytes,
-                        int band_height, int n_ranks, int slab_rows, void* stream) {
-    if (!gathered || !image) return rt_fail(RT_EINVAL, "rt_unshuffle_dev: null buffer");
+static int check_band_geometry(const char* who, const void* gathered, const void* image, int W, int H,
+                               int band_height, int n_ranks, int slab_rows) {
+    if (!gathered || !image) return rt_fail(RT_EINVAL, std::string(who) + ": null buffer");
     if (W <= 0 || H <= 0 || band_height <= 0 || n_ranks <= 0 || slab_rows < 0)
-        return rt_fail(RT_EINVAL, "rt_unshuffle_dev: bad geometry");
-    if (elem_bytes <= 0 || ((long long)W * elem_bytes) % 4 != 0)
-        return rt_fail(RT_EINVAL, "rt_unshuffle_dev: row bytes must be a multiple of 4");
+        return rt_fail(RT_EINVAL, std::string(who) + ": bad geometry");
     rt_rows r = {band_height, n_ranks, 0, 0};
     for (int q = 0; q < n_ranks; ++q) {
         int nl = 0;
         r.rank = q;
         rt_local_rows(H, &r, &nl);
-        if (nl > slab_rows) return rt_fail(RT_EINVAL, "rt_unshuffle_dev: slab_rows smaller than a rank's rows");
+        if (nl > slab_rows) return rt_fail(RT_EINVAL, std::string(who) + ": slab_rows smaller than a rank's rows");
     }
+    return RT_OK;
+}
+
+int rt_unshuffle_dev_ex(const void* gathered, const void* rank0_slab, void* image, int W, int H, int elem_bytes,
+                        int band_height, int n_ranks, int slab_rows, void* stream) {
+    int rc = check_band_geometry("rt_unshuffle_dev", gathered, image, W, H, band_height, n_ranks, slab_rows);
+    if (rc) return rc;
+    if (elem_bytes <= 0 || ((long long)W * elem_bytes) % 4 != 0)
+        return rt_fail(RT_EINVAL, "rt_unshuffle_dev: row bytes must be a multiple of 4");
     const int row_words = (int)(((long long)W * elem_bytes) / 4);
     const bool vec = row_words % 4 == 0 && ((uintptr_t)gathered | (uintptr_t)rank0_slab | (uintptr_t)image) % 16 == 0;
     auto k = vec ? rt_unshuffle_kernel<4> : rt_unshuffle_kernel<1>;
@@ -985,6 +1030,44 @@ extern "C" int rt_unshuffle_dev(const void* gathered, void* image, int W, int H,
     return rt_unshuffle_dev_ex(gathered, nullptr, image, W, H, elem_bytes, band_height, n_ranks, slab_rows, stream);
 }
 
+int rt_unpack_dev_ex(const void* gathered, const void* rank0_slab, void* image, int W, int H, int src_format,
+                     int dst_format, int band_height, int n_ranks, int slab_rows, void* stream) {
+    int sb = 0, db = 0;
+    int rc = rt_pixel_bytes(src_format, &sb);
+    if (!rc) rc = rt_pixel_bytes(dst_format, &db);
+    if (rc) return rc;
+    if (src_format == dst_format)
+        return rt_unshuffle_dev_ex(gathered, rank0_slab, image, W, H, sb, band_height, n_ranks, slab_rows, stream);
+    rc = check_band_geometry("rt_unpack_dev", gathered, image, W, H, band_height, n_ranks, slab_rows);
+    if (rc) return rc;
+    int mode;
+    if (src_format == RT_PIXEL_GRAY8 && dst_format == RT_PIXEL_RGBA8) mode = kUnpackGray8;
+    else if (src_format == RT_PIXEL_RGB8 && dst_format == RT_PIXEL_RGBA8) mode = kUnpackRgb8;
+    else if (src_format == RT_PIXEL_GRAY32F && dst_format == RT_PIXEL_RGBA32F) mode = kUnpackGray32f;
+    else return rt_fail(RT_EINVAL, "rt_unpack_dev: unsupported format pair");
+    const bool vec = W % 4 == 0 && ((uintptr_t)gathered | (uintptr_t)rank0_slab | (uintptr_t)image) % 16 == 0;
+    const uint8_t* g = (const uint8_t*)gathered;
+    const uint8_t* g0 = (const uint8_t*)rank0_slab;
+    uint8_t* im = (uint8_t*)image;
+    const hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)H), blk(kThreads);
+#define RT_UNPACK(M, V) hipLaunchKernelGGL((rt_unpack_kernel<M, V>), grid, blk, 0, st, g, g0, im, W, H, band_height, \
+                                           n_ranks, slab_rows)
+    if (mode == kUnpackGray8) { if (vec) RT_UNPACK(kUnpackGray8, true); else RT_UNPACK(kUnpackGray8, false); }
+    else if (mode == kUnpackRgb8) { if (vec) RT_UNPACK(kUnpackRgb8, true); else RT_UNPACK(kUnpackRgb8, false); }
+    else { if (vec) RT_UNPACK(kUnpackGray32f, true); else RT_UNPACK(kUnpackGray32f, false); }
+#undef RT_UNPACK
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_unpack_kernel: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+extern "C" int rt_unpack_dev(const void* gathered, void* image, int W, int H, int src_format, int dst_format,
+                             int band_height, int n_ranks, int slab_rows, void* stream) {
+    return rt_unpack_dev_ex(gathered, nullptr, image, W, H, src_format, dst_format, band_height, n_ranks, slab_rows,
+                            stream);
+}
+
 // Diagnostics (include/rt_diag.h): tile-row dispatch order of later renders: 0 adaptive (default), 1
 // bottom-to-top.
 extern "C" int rt_diag_tile_order(rt_ctx* c, int mode) {
@@ -998,35 +1081,21 @@ extern "C" int rt_diag_tile_order(rt_ctx* c, int mode) {
 // Diagnostics (include/rt_diag.h): registers and scratch of the render kernel instance rt_render_dev
 // launches for `depth` and scene kind `variant` (0 spheres + board, 1 >= kConeMin spheres (CULL),
 // 2 meshes / transparency, 3 ray trees) — the tests assert the default instances never spill.
-template <int B>
-static const void* render_kernel_of(int variant) {
-    constexpr int kFast = B <= 3 ? (RT_MINW != 0 ? RT_MINW : (B <= 2 ? 6 : 5)) : 1;
-    constexpr int kCull = B <= 3 ? RT_MINW_CULL : 1;
-    switch (variant) {
-        case 0: return (const void*)rt_render_kernel<B, 0, kFast, false, false, RT_WG_FAST, false>;
-        case 1: return (const void*)rt_render_kernel<B, 0, kCull, false, true, RT_WG_FAST, false>;
-        case 2: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, false>;
-        case 3: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, true>;
-        default: return nullptr;
-    }
-}
-
 extern "C" int rt_diag_kernel_resources(int depth, int variant, int* vgprs, int* scratch_bytes) {
     if (depth < 0 || depth > RT_MAX_B || variant < 0 || variant > 3 || !vgprs || !scratch_bytes)
         return rt_fail(RT_EINVAL, "rt_diag_kernel_resources: bad arguments");
     const void* f = nullptr;
     switch (depth) {
-        case 0: f = render_kernel_of<0>(variant); break;
-        case 1: f = render_kernel_of<1>(variant); break;
-        case 2: f = render_kernel_of<2>(variant); break;
-        case 3: f = render_kernel_of<3>(variant); break;
-#if RT_MAX_B >= 7
-        case 4: f = render_kernel_of<4>(variant); break;
-        case 5: f = render_kernel_of<5>(variant); break;
-        case 6: f = render_kernel_of<6>(variant); break;
-        case 7: f = render_kernel_of<7>(variant); break;
-#endif
+        case 0: f = render_kernel_ptr<0>(variant); break;
+        case 1: f = render_kernel_ptr<1>(variant); break;
+        case 2: f = render_kernel_ptr<2>(variant); break;
+        case 3: f = render_kernel_ptr<3>(variant); break;
+        case 4: f = render_kernel_ptr<4>(variant); break;
+        case 5: f = render_kernel_ptr<5>(variant); break;
+        case 6: f = render_kernel_ptr<6>(variant); break;
+        default: f = render_kernel_ptr<7>(variant); break;
     }
+    if (!f) return rt_fail(RT_EINVAL, "rt_diag_kernel_resources: kernel not built");
     hipFuncAttributes a;
     RT_HIP(hipFuncGetAttributes(&a, f));
     *vgprs = a.numRegs;

@@ -110,6 +110,7 @@ struct alignas(16) DevScene {
     double board_skip_y;               // rays starting at a board hit whose ray came from |y| <= this provably
                                        // miss the board (rt_device.hpp origin_skip); -1: never skipped
     double self_eps2;                  // eps^2 / 4: sphere self-test skip threshold (origin_skip)
+    double hits_lim2;                  // hits_inside holds for rays whose level-0 origin o has |o - bc|^2 <= this
     double board_num;                  // n . (v0 - eye) of the board plane for the camera `eye` (per eye)
     double eye[3];                     // camera the *Prim arrays and board_num were computed for
     int32_t bound_on;                  // g_scene radius > 0
@@ -123,7 +124,7 @@ struct alignas(16) DevScene {
     int32_t transparent;               // some material is transparent: closest-hit shadows, weighted children
     int32_t tree;                      // some material transmits AND reflects: ray-tree kernels (trace_tree)
     int32_t hits_inside;               // every hit point lies within (R - 1) of bc: rays from hits pass the cull
-    int32_t pad1;
+    int32_t hits_ok;                   // hits_inside for the camera eye (rt_prepare_kernel, per eye)
     DevTri tri[2];                     // board triangles T1 = (P1,P2,P3), T2 = (P1,P3,P4)   (:840-841)
     DevMat mat[5];                     // 0 white square, 1 black square, 2 sphere, 3 tetrahedron, 4 cube
     DevLight light[16];

@@ -1,0 +1,456 @@
+// rt_render.hpp — the per-pixel render kernel and the ray-list kernel (templates), shared by rt_kernel.hip
+// (the C ABI) and the per-depth instance files rt_render_b<B>.hip.  The bounce depth B is a template
+// parameter (the bounce loop is unrolled); each depth's instances live in their own translation unit so the
+// eight depths compile in parallel (one file with all of them took > 5 minutes of one core).
+//
+//   rt_render_kernel<B, LDS, MINW, TRANSP, CULL, WG, TREE>  one work-item per pixel, FP64, iterative bounce
+//                             loop (rt_device.hpp).  Default: one-wave workgroups (WG = 64), each owning an
+//                             8 x 8 pixel tile (square tiles keep a wave's rays coherent, so the __any early-out
+//                             and the culling masks work for whole waves).  The scene is read through the
+//                             scalar cache; the A/B variants with 256-thread workgroups (32 x 8 tiles) copy it
+//                             into LDS once per workgroup (LDS = 1) or stage the output tile in LDS for 32-pixel
+//                             row stores.  Per-level colours wait in LDS slots; stores go out per wave.
+//   rt_trace_rays_kernel<B>   rayTraceRay on an arbitrary ray list (parity / fuzz / faithful-screen entry).
+//
+// Output pixel formats (RenderParams::fmt_f / fmt_8, wave-uniform): the float image is RGBA32F (16 B/px) or
+// GRAY32F (4 B/px, the R channel: only for scenes proven achromatic, where R = G = B bit for bit); the byte
+// image is RGBA8 (4 B/px), RGB8 (3 B/px) or GRAY8 (1 B/px, achromatic scenes).  The packed formats cut the
+// bytes a frame moves over xGMI (rt_render_multi) or PCIe (rt_render_packed).
+//
+// Reference: /root/reference/Hw4/MySdlApplication.cpp (rayTraceScreen :1251-1324, rayTraceRay :1184-1249,
+// intersection code :611-823, :1084-1113).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/rt_api.h"
+#include "rt_device.hpp"
+
+#ifndef RT_WAVE_TRACE
+#define RT_WAVE_TRACE 0
+#endif
+// __launch_bounds__ minimum waves per EU of the depth <= 3 render kernels.  0 (default): 6 for depth <= 2
+// (<= 80 VGPRs, no spills since the bounce loop stopped carrying the previous ray through the light loop),
+// 5 for depth 3 (<= 96 VGPRs; 6 would spill 8 B/lane).
+#ifndef RT_MINW
+#define RT_MINW 0
+#endif
+#ifndef RT_NT_STORES
+#define RT_NT_STORES 0                         // 1: non-temporal RGBA32F/RGBA8 stores (A/B)
+#endif
+#ifndef RT_WG_FAST
+#define RT_WG_FAST 64                          // workgroup of the default render kernels: 64 (8 x 8) or 128 (16 x 8)
+#endif
+#ifndef RT_MINW_CULL
+#define RT_MINW_CULL 5                         // the culling variant (>= kConeMin spheres): 87 VGPRs, no spills
+#endif
+// RT_MAX_B < 7 (experiment builds only, tools/variants.sh): deeper kernels are not instantiated.
+#ifndef RT_MAX_B
+#define RT_MAX_B 7
+#endif
+
+namespace rtk {
+
+using namespace rt;
+
+constexpr int kTileW = 32;   // workgroup tile of the 256-thread variants: 32 columns ...
+constexpr int kTileH = 8;    // ... x 8 rows = 256 pixels
+constexpr int kThreads = 256;
+static_assert(kThreads == kSlotStride, "one LDS colour slot column per work-item");
+constexpr int kGridY = 32768;                  // grid.y per grid.z slice
+
+// Pixel formats of the kernel's two images (include/rt_api.h RT_PIXEL_*).
+constexpr int kFmtF_RGBA = 0, kFmtF_GRAY = 1;                // float image
+constexpr int kFmt8_RGBA = 0, kFmt8_RGB = 1, kFmt8_GRAY = 2;  // byte image
+
+// LDS bytes of trace()'s per-level slots for depth B: 3 doubles (+ the material id when TRANSP) per level
+// and work-item of a `wg`-thread workgroup.
+__host__ __device__ constexpr int slot_bytes(int B, bool transp, int wg = kSlotStride) {
+    return (B + 1) * (3 * 8 + (transp ? 4 : 0)) * wg;
+}
+
+struct RenderParams {
+    double eye[3];
+    double look[3];
+    double right[3];
+    double upp[3];
+    double pitch;
+    int32_t bottom_x, bottom_y;
+    int32_t width, height;
+    int32_t local_rows;                        // over all frames
+    int32_t frame_rows;                        // local rows per frame
+    int32_t frames;
+    int32_t band_height, n_ranks, rank;
+    int32_t lds_bytes;
+    int32_t np;
+    int32_t nl;
+    int32_t wg_staging;                        // 1: stage the 32 x 8 tile in LDS behind a workgroup barrier
+    int32_t fmt_f;                             // kFmtF_*: float image format
+    int32_t fmt_8;                             // kFmt8_*: byte image format
+    float look32[3], right32[3], upp32[3], eye32[3], pitch32;   // FP32 camera for primary_cone_mask
+    float cone_slack;                          // its error bound (render_params)
+    const int32_t* tile_rows;                  // dispatch order of tile rows (nullptr: bottom to top)
+    uint32_t* row_cost;                        // calibration render: per tile row, sum of wave times (100 MHz)
+    int32_t tile_rows_n;                       // tile rows of this launch
+    uint64_t* wtrace;                          // RT_WAVE_TRACE builds: per-wave {start, end, HW_ID}
+};
+
+// Image row (within its frame) of local row lr; local rows are frame-major (rt_rows.frames).
+__device__ __forceinline__ int global_row_of(const RenderParams& P, int lr) {
+    if (P.frames > 1) lr %= P.frame_rows;
+    if (P.n_ranks <= 1) return lr;
+    int band = lr / P.band_height, within = lr - band * P.band_height;
+    return (band * P.n_ranks + P.rank) * P.band_height + within;
+}
+
+// Copy the scene record into LDS, 16 B per work-item per step.
+__device__ __forceinline__ void stage_scene(char* dst, const DevScene* __restrict__ src, int bytes) {
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    for (int k = threadIdx.x; k < (bytes >> 4); k += kThreads) d[k] = s[k];
+}
+
+// floor(clamp(c, 0, 1) * 255 + 0.5) (RGBA8 definition).  fmax/fmin (v_max/v_min_f64) clamp
+// exactly like the comparisons; NaN becomes 0 (the conversion of a NaN is 0 on the device as well).
+__device__ __forceinline__ unsigned char to_u8(double c) {
+    double v = fmin(fmax(c, 0.0), 1.0);
+    return (unsigned char)(int)floor(v * 255.0 + 0.5);
+}
+
+// Store pixel k of the two images in their formats.  PACKED = false: RGBA32F / RGBA8 only (the benchmark
+// kernels: the runtime format branches cost c3 8% through the whole kernel's register allocation, same-box
+// A/B); PACKED = true: fmt_f / fmt_8 are kernel arguments (scalar branches).
+template <bool PACKED>
+__device__ __forceinline__ void store_pixel(const RenderParams& P, size_t k, d3 col, void* __restrict__ out32,
+                                            void* __restrict__ out8) {
+    if (out32) {
+        if (PACKED && P.fmt_f == kFmtF_GRAY) {
+            reinterpret_cast<float*>(out32)[k] = (float)col.x;
+        } else {
+#if RT_NT_STORES
+            float* o = reinterpret_cast<float*>(out32) + 4 * k;
+            __builtin_nontemporal_store((float)col.x, o);
+            __builtin_nontemporal_store((float)col.y, o + 1);
+            __builtin_nontemporal_store((float)col.z, o + 2);
+            __builtin_nontemporal_store(1.0f, o + 3);
+#else
+            reinterpret_cast<float4*>(out32)[k] = make_float4((float)col.x, (float)col.y, (float)col.z, 1.0f);
+#endif
+        }
+    }
+    if (out8) {
+        if (PACKED && P.fmt_8 == kFmt8_GRAY) {
+            reinterpret_cast<uint8_t*>(out8)[k] = to_u8(col.x);
+        } else if (PACKED && P.fmt_8 == kFmt8_RGB) {
+            uint8_t* o = reinterpret_cast<uint8_t*>(out8) + 3 * k;
+            o[0] = to_u8(col.x);
+            o[1] = to_u8(col.y);
+            o[2] = to_u8(col.z);
+        } else {
+#if RT_NT_STORES
+            const uint32_t px = (uint32_t)to_u8(col.x) | ((uint32_t)to_u8(col.y) << 8) |
+                                ((uint32_t)to_u8(col.z) << 16) | (255u << 24);
+            __builtin_nontemporal_store(px, reinterpret_cast<uint32_t*>(out8) + k);
+#else
+            reinterpret_cast<uchar4*>(out8)[k] = make_uchar4(to_u8(col.x), to_u8(col.y), to_u8(col.z), 255);
+#endif
+        }
+    }
+}
+
+template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false,
+          bool PACKED = false>
+__global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
+                                                             RenderParams P, void* __restrict__ out32,
+                                                             void* __restrict__ out8,
+                                                             double* __restrict__ out64,
+                                                             uint32_t* __restrict__ outrc) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x;
+#if RT_WAVE_TRACE
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    const uint64_t t_cal = P.row_cost ? __builtin_amdgcn_s_memrealtime() : 0;
+    // LDS: [header | DevSphere[np] | DevSpherePrim[np]] (LDS = 1), the per-level colour slots of trace()
+    // (slot_bytes), then the output staging tile (12 KB, RT_WG_STAGING only).
+    // The scene record is broadcast into LDS once per workgroup; the FP32 filter images stay in global
+    // memory and are read with wave-uniform indices (scalar loads, SGPR operands).
+    int off = 0;
+    const DevScene* S = gscene;
+    if (LDS) {
+        stage_scene(smem, gscene, P.lds_bytes);
+        S = reinterpret_cast<const DevScene*>(smem);
+        off = P.lds_bytes;
+    }
+    double* slot = reinterpret_cast<double*>(smem + off) + tid;
+    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * (B + 1) * WG) + tid;
+    off += slot_bytes(B, TRANSP, WG);
+    float4* st32 = reinterpret_cast<float4*>(smem + off);                              // [8][32] 4 KB
+    double* st64 = reinterpret_cast<double*>(smem + off + 4096);                        // [8][32][3] 6 KB
+    uint32_t* strc = reinterpret_cast<uint32_t*>(smem + off + 4096 + 6144);             // [8][32] 1 KB
+    uchar4* st8 = reinterpret_cast<uchar4*>(smem + off + 4096 + 6144 + 1024);           // [8][32] 1 KB
+    if (LDS) __syncthreads();
+    const SceneView V = view_of(S, gscene, P.np, P.nl);
+    const d3 eye = ld3(P.eye);
+
+    const int wave = tid >> 6, lane = tid & 63;
+    // The 32 x 8 tile (WG = 256) is cut into 4 wave blocks of 8 x 8 pixels (square blocks keep a wave's
+    // rays coherent; 16 x 4 and 32 x 2 blocks measured no faster, and 32 x 2 slower at c5); WG = 64: one
+    // wave, one 8 x 8 tile.
+    constexpr int bw = 8, bh = 8, TW = WG / 8;
+    const int bx0 = wave * bw, by0 = 0;
+    const int cx = bx0 + (lane & 7);               // column inside the tile
+    const int cy = lane >> 3;                      // row inside the tile
+    const int tx = blockIdx.x;                      // 2-D grid: tiles_x x tiles_y
+    const int gy = (int)(blockIdx.z * kGridY + blockIdx.y);    // tile rows beyond kGridY go to grid.z
+    const int ty = P.tile_rows ? P.tile_rows[gy] : gy;
+    if ((unsigned)ty >= (unsigned)P.tile_rows_n) return;        // padding of the last grid.z slice
+    const int i = tx * TW + cx;
+    const int lr = ty * kTileH + cy;
+    const bool valid = i < P.width && lr < P.local_rows;
+
+    // Per-wave sphere culling (all lanes active here).  The block's rows must be contiguous image rows.
+    uint64_t cone = ~0ull;
+    if (P.np >= kConeMin) {
+        // Within one frame global_row_of is increasing, so jb - ja == 7 means 8 consecutive rows.
+        const int lr0 = ty * kTileH + by0, ja = global_row_of(P, lr0), jb = global_row_of(P, lr0 + bh - 1);
+        const bool one_frame = P.frames <= 1 || lr0 / P.frame_rows == (lr0 + bh - 1) / P.frame_rows;
+        const float hx = 0.5f * (float)(bw - 1), hy = 0.5f * (float)(bh - 1);
+        if (one_frame && jb - ja == bh - 1)
+            cone = primary_cone_mask(V, P.look32, P.right32, P.upp32, P.eye32, P.pitch32,
+                                     (float)(tx * TW + bx0 + P.bottom_x) + hx, (float)(ja + P.bottom_y) + hy,
+                                     sqrtf(hx * hx + hy * hy), P.cone_slack, lane);
+    }
+
+    // Every lane traces (trace() reduces over the wave): lanes outside the frame trace a clamped pixel
+    // and store nothing.
+    uint32_t seg = 0, sh = 0;
+    const int ic = i < P.width ? i : P.width - 1, lrc = lr < P.local_rows ? lr : P.local_rows - 1;
+    const int j = global_row_of(P, lrc);
+    const d3 right = ld3(P.right), upp = ld3(P.upp);
+    // Primary ray Line(camera, sp), SURVEY.md Appendix B (basis: rayTraceScreen :1270-1279).
+    const d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(ic + P.bottom_x), right)),
+                      scl(P.pitch * (double)(j + P.bottom_y), upp));
+    const d3 bdP = sub(ld3(V.S->bc), eye);                  // bounding-sphere deltaP for p0 = camera
+    d3 col;
+    if constexpr (TREE)
+        col = trace_tree<B>(V, eye, sp, &seg, &sh);
+    else
+        col = trace<B, true, TRANSP, CULL, WG>(V, eye, sp, bdP, dot(bdP, bdP), cone, &seg, &sh, slot, mslot);
+
+    if (WG != kThreads || !P.wg_staging) {
+        // Direct stores: each wave writes its 8 x 8 block as 8 row segments (128 B of RGBA32F each) and
+        // retires without waiting at a workgroup barrier for slower waves of the tile.
+        if (valid) {
+            const size_t k = (size_t)lr * P.width + i;
+            store_pixel<PACKED>(P, k, col, out32, out8);
+            if (out64) { out64[3 * k] = col.x; out64[3 * k + 1] = col.y; out64[3 * k + 2] = col.z; }
+            if (outrc) outrc[k] = seg | (sh << 16);
+        }
+        if (P.row_cost && tid == 0)
+            atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
+#if RT_WAVE_TRACE
+        if (P.wtrace && tid == 0) {
+            const size_t w = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+            P.wtrace[3 * w] = t_start;
+            P.wtrace[3 * w + 1] = __builtin_amdgcn_s_memrealtime();
+            P.wtrace[3 * w + 2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                                  ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
+        }
+#endif
+        return;
+    }
+    // Stage through LDS, then store whole tile rows (RGBA formats only: the host routes packed formats to the
+    // direct-store variants).
+    const int ts = cy * kTileW + cx;
+    if (out32) st32[ts] = make_float4((float)col.x, (float)col.y, (float)col.z, 1.0f);
+    if (out64) { st64[3 * ts] = col.x; st64[3 * ts + 1] = col.y; st64[3 * ts + 2] = col.z; }
+    if (outrc) strc[ts] = seg | (sh << 16);
+    if (out8) st8[ts] = make_uchar4(to_u8(col.x), to_u8(col.y), to_u8(col.z), 255);
+    __syncthreads();
+    const int oy = tid >> 5, ox = tid & 31;
+    const int gi = tx * kTileW + ox, glr = ty * kTileH + oy;
+    if (gi < P.width && glr < P.local_rows) {
+        const size_t k = (size_t)glr * P.width + gi;
+        if (out32) reinterpret_cast<float4*>(out32)[k] = st32[tid];
+        if (out64) {
+            out64[3 * k] = st64[3 * tid];
+            out64[3 * k + 1] = st64[3 * tid + 1];
+            out64[3 * k + 2] = st64[3 * tid + 2];
+        }
+        if (outrc) outrc[k] = strc[tid];
+        if (out8) reinterpret_cast<uchar4*>(out8)[k] = st8[tid];
+    }
+    if (P.row_cost && tid == 0) atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
+}
+
+// rayTraceRay on a list of rays Line(starts[k], ends[k]).  Rays from arbitrary starts: whether their hit
+// points may skip the bounding-sphere cull is decided per ray (hits_ok_from).
+template <int B, bool TRANSP, bool TREE = false>
+__global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene* __restrict__ S,
+                                                                 const double* __restrict__ starts,
+                                                                 const double* __restrict__ ends, int n,
+                                                                 double* __restrict__ rgb,
+                                                                 uint32_t* __restrict__ rc) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // Every lane traces (trace() reduces over the wave); lanes past n repeat ray n - 1 and store nothing.
+    const int k = blockIdx.x * kThreads + threadIdx.x, kk = k < n ? k : n - 1;
+    uint32_t seg = 0, sh = 0;
+    SceneView V = view_of(S, S, S->n_padded, S->n_lights);
+    const d3 p0 = ld3(starts + 3 * kk);
+    V.hits_ok = hits_ok_from(S, p0);
+    double* slot = reinterpret_cast<double*>(smem) + threadIdx.x;
+    int* mslot = reinterpret_cast<int*>(smem + 3 * 8 * (B + 1) * kSlotStride) + threadIdx.x;
+    d3 c;
+    if constexpr (TREE)
+        c = trace_tree<B>(V, p0, ld3(ends + 3 * kk), &seg, &sh);
+    else
+        c = trace<B, false, TRANSP, false>(V, p0, ld3(ends + 3 * kk), mk(0.0, 0.0, 0.0), 0.0, ~0ull, &seg, &sh, slot,
+                                           mslot);
+    if (k >= n) return;
+    if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
+    if (rc) rc[k] = seg | (sh << 16);
+}
+
+// Render-kernel variants rt_render_dev chooses between (rt_kernel.hip).
+enum RenderVariant {
+    kVarFast = 0,          // spheres + board (the benchmark kernels), launch bounds RT_MINW (depth <= 3)
+    kVarFastAnyW,          // ... no occupancy bound (depth > 3, or RT_MIN_WAVES < 5)
+    kVarCull,              // >= kConeMin spheres: per-wave culling, RT_MINW_CULL (depth <= 3)
+    kVarCullAnyW,
+    kVarTransp,            // meshes / transparent materials (FULL)
+    kVarTree,              // ray trees (trace_tree)
+    kVarLds,               // A/B: scene in LDS, 256-thread workgroups
+    kVarStaging,           // A/B: LDS-staged row stores, 256-thread workgroups, RT_MINW
+    kVarStagingAnyW,
+    // packed pixel formats (rt_render_dev_packed: GRAY / RGB images), one per scene kind
+    kVarFastPacked,
+    kVarCullPacked,
+    kVarTranspPacked,
+    kVarTreePacked,
+    kVarCount
+};
+
+struct RenderLaunch {
+    int variant;
+    dim3 grid;
+    size_t lds;
+    hipStream_t stream;
+    const DevScene* scene;
+    RenderParams P;
+    void* o32;
+    void* o8;
+    double* o64;
+    uint32_t* orc;
+};
+
+// Defined once per depth B in rt_render_b<B>.hip.
+template <int B>
+hipError_t launch_render(const RenderLaunch& L);
+template <int B>
+hipError_t launch_trace_rays(int variant /* 0 opaque, 1 FULL, 2 tree */, dim3 grid, hipStream_t st,
+                             const DevScene* s, const double* a, const double* b, int n, double* rgb, uint32_t* rc);
+template <int B>
+const void* render_kernel_ptr(int variant);   // rt_diag_kernel_resources: 0 fast, 1 cull, 2 FULL, 3 tree
+
+#define RT_DECLARE_DEPTH(B)                                                                                   \
+    template <>                                                                                                \
+    hipError_t launch_render<B>(const RenderLaunch& L);                                                        \
+    template <>                                                                                                \
+    hipError_t launch_trace_rays<B>(int, dim3, hipStream_t, const DevScene*, const double*, const double*, int,   \
+                                    double*, uint32_t*);                                                       \
+    template <>                                                                                                \
+    const void* render_kernel_ptr<B>(int);
+RT_DECLARE_DEPTH(0) RT_DECLARE_DEPTH(1) RT_DECLARE_DEPTH(2) RT_DECLARE_DEPTH(3)
+RT_DECLARE_DEPTH(4) RT_DECLARE_DEPTH(5) RT_DECLARE_DEPTH(6) RT_DECLARE_DEPTH(7)
+#undef RT_DECLARE_DEPTH
+
+// Body of the per-depth instance files.
+template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG, bool TREE, bool PACKED = false>
+hipError_t launch_render_one(const RenderLaunch& L) {
+    auto kern = rt_render_kernel<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED>;
+    if (L.lds > 65536) {
+        hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, L.grid, dim3(WG), L.lds, L.stream, L.scene, L.P, L.o32, L.o8, L.o64, L.orc);
+    return hipGetLastError();
+}
+
+template <int B>
+hipError_t launch_render_impl(const RenderLaunch& L) {
+    if constexpr (B > RT_MAX_B) {
+        return hipErrorInvalidValue;
+    } else {
+        constexpr int MW = RT_MINW != 0 ? RT_MINW : (B <= 2 ? 6 : 5);     // depth-dependent default
+        switch (L.variant) {
+            case kVarFast: return launch_render_one<B, 0, MW, false, false, RT_WG_FAST, false>(L);
+            case kVarFastAnyW: return launch_render_one<B, 0, 1, false, false, RT_WG_FAST, false>(L);
+            case kVarCull: return launch_render_one<B, 0, RT_MINW_CULL, false, true, RT_WG_FAST, false>(L);
+            case kVarCullAnyW: return launch_render_one<B, 0, 1, false, true, RT_WG_FAST, false>(L);
+            case kVarTransp: return launch_render_one<B, 0, 1, true, false, 64, false>(L);
+            case kVarTree: return launch_render_one<B, 0, 1, true, false, 64, true>(L);
+            case kVarLds: return launch_render_one<B, 1, 1, false, false, kThreads, false>(L);
+            case kVarStaging: return launch_render_one<B, 0, MW, false, false, kThreads, false>(L);
+            case kVarStagingAnyW: return launch_render_one<B, 0, 1, false, false, kThreads, false>(L);
+            case kVarFastPacked:
+                return launch_render_one<B, 0, (B <= 3 ? MW : 1), false, false, RT_WG_FAST, false, true>(L);
+            case kVarCullPacked:
+                return launch_render_one<B, 0, (B <= 3 ? RT_MINW_CULL : 1), false, true, RT_WG_FAST, false, true>(L);
+            case kVarTranspPacked: return launch_render_one<B, 0, 1, true, false, 64, false, true>(L);
+            case kVarTreePacked: return launch_render_one<B, 0, 1, true, false, 64, true, true>(L);
+            default: return hipErrorInvalidValue;
+        }
+    }
+}
+
+template <int B>
+hipError_t launch_trace_rays_impl(int variant, dim3 grid, hipStream_t st, const DevScene* s, const double* a,
+                                  const double* b, int n, double* rgb, uint32_t* rc) {
+    if constexpr (B > RT_MAX_B) {
+        return hipErrorInvalidValue;
+    } else {
+        if (variant == 2)
+            hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, true>), grid, dim3(kThreads), 0, st, s, a, b, n, rgb, rc);
+        else if (variant == 1)
+            hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, false>), grid, dim3(kThreads), slot_bytes(B, true), st, s,
+                               a, b, n, rgb, rc);
+        else
+            hipLaunchKernelGGL((rt_trace_rays_kernel<B, false, false>), grid, dim3(kThreads), slot_bytes(B, false), st,
+                               s, a, b, n, rgb, rc);
+        return hipGetLastError();
+    }
+}
+
+template <int B>
+const void* render_kernel_ptr_impl(int variant) {
+    if constexpr (B > RT_MAX_B) {
+        return nullptr;
+    } else {
+        constexpr int kFast = B <= 3 ? (RT_MINW != 0 ? RT_MINW : (B <= 2 ? 6 : 5)) : 1;
+        constexpr int kCull = B <= 3 ? RT_MINW_CULL : 1;
+        switch (variant) {
+            case 0: return (const void*)rt_render_kernel<B, 0, kFast, false, false, RT_WG_FAST, false>;
+            case 1: return (const void*)rt_render_kernel<B, 0, kCull, false, true, RT_WG_FAST, false>;
+            case 2: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, false>;
+            case 3: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, true>;
+            default: return nullptr;
+        }
+    }
+}
+
+}  // namespace rtk
+
+// One line per instance file: the depth-B definitions of the three declarations above.
+#define RT_RENDER_INSTANCES(B)                                                                                  \
+    namespace rtk {                                                                                            \
+    template <>                                                                                                \
+    hipError_t launch_render<B>(const RenderLaunch& L) { return launch_render_impl<B>(L); }                    \
+    template <>                                                                                                \
+    hipError_t launch_trace_rays<B>(int v, dim3 g, hipStream_t st, const DevScene* s, const double* a,         \
+                                    const double* b, int n, double* rgb, uint32_t* rc) {                       \
+        return launch_trace_rays_impl<B>(v, g, st, s, a, b, n, rgb, rc);                                       \
+    }                                                                                                          \
+    template <>                                                                                                \
+    const void* render_kernel_ptr<B>(int v) { return render_kernel_ptr_impl<B>(v); }                           \
+    }

@@ -75,6 +75,27 @@ class Tracer:
         bufs = self.alloc(width, height, rows, rgba32f, rgba8, rgb64f, raycount)
         return self.render_into(cam, width, height, depth, bufs, rows, stream)
 
+    def render_packed(self, cam, width, height, depth, float_format=None, byte_format=None, rows=None,
+                      stream=None):
+        """rt_render_dev_packed: the float image in float_format (RT_PIXEL_RGBA32F / GRAY32F) and the byte
+        image in byte_format (RT_PIXEL_RGBA8 / RGB8 / GRAY8), each None to skip.  Returns (float, byte)
+        tensors of shape (rows, W, channels)."""
+        nl = scenes.local_rows(height, rows)
+        dev = torch.device("cuda", self.device)
+        ch = {abi.RT_PIXEL_RGBA32F: 4, abi.RT_PIXEL_GRAY32F: 1, abi.RT_PIXEL_RGBA8: 4, abi.RT_PIXEL_RGB8: 3,
+              abi.RT_PIXEL_GRAY8: 1}
+        f = torch.empty((nl, width, ch[float_format]), dtype=torch.float32, device=dev) if float_format is not None \
+            else None
+        b = torch.empty((nl, width, ch[byte_format]), dtype=torch.uint8, device=dev) if byte_format is not None \
+            else None
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        abi.check(abi.lib().rt_render_dev_packed(
+            self._ctx, ctypes.byref(cam), width, height, depth, ctypes.byref(rows) if rows is not None else None,
+            float_format if float_format is not None else abi.RT_PIXEL_RGBA32F, _ptr(f),
+            byte_format if byte_format is not None else abi.RT_PIXEL_RGBA8, _ptr(b),
+            ctypes.c_void_p(st.cuda_stream)), "rt_render_dev_packed")
+        return f, b
+
     def render_host(self, scene_abi, cam, width, height, depth, rows=None):
         """rt_render (host buffers, synchronous) -> (rgb64f numpy, rt_stats)."""
         import numpy as np
@@ -112,6 +133,15 @@ def unshuffle(gathered: torch.Tensor, image: torch.Tensor, width: int, height: i
     st = stream if stream is not None else torch.cuda.current_stream(image.device)
     abi.check(abi.lib().rt_unshuffle_dev(_ptr(gathered), _ptr(image), width, height, elem, band_height, n_ranks,
                                          slab_rows, ctypes.c_void_p(st.cuda_stream)), "rt_unshuffle_dev")
+    return image
+
+
+def unpack(gathered: torch.Tensor, image: torch.Tensor, width: int, height: int, src_format: int, dst_format: int,
+           band_height: int, n_ranks: int, slab_rows: int, stream=None):
+    """rt_unpack_dev: packed slabs (src_format) -> image (dst_format), bands put in image order."""
+    st = stream if stream is not None else torch.cuda.current_stream(image.device)
+    abi.check(abi.lib().rt_unpack_dev(_ptr(gathered), _ptr(image), width, height, src_format, dst_format, band_height,
+                                      n_ranks, slab_rows, ctypes.c_void_p(st.cuda_stream)), "rt_unpack_dev")
     return image
 
 

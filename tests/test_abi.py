@@ -192,3 +192,53 @@ def test_integration_snippet_is_the_built_dropin():
     assert len(lines) > 20
     missing = [x for x in lines if x not in src_lines]
     assert not missing, missing
+
+
+def test_pixel_formats_and_group_stats_layout():
+    L = abi.lib()
+    for f, nb in abi.PIXEL_BYTES.items():
+        b = ctypes.c_int()
+        abi.check(L.rt_pixel_bytes(f, ctypes.byref(b)), "rt_pixel_bytes")
+        assert b.value == nb
+    assert L.rt_pixel_bytes(9, ctypes.byref(ctypes.c_int())) == abi.RT_EINVAL
+    assert ctypes.sizeof(abi.rt_group_stats) == 4 * 4 + 8 + 4 * 8
+
+
+def _achromatic(sc) -> int:
+    out = ctypes.c_int(-1)
+    abi.check(abi.lib().rt_scene_achromatic(ctypes.byref(sc), ctypes.byref(out)), "rt_scene_achromatic")
+    return out.value
+
+
+def test_scene_achromatic_rule():
+    """GRAY formats are exact only when every material term the objects use and every light colour has equal
+    components (MSA:577, 583-588).  The canonical scenes and the app's tetrahedron are; its red cube is not —
+    and an unused red cube material does not matter."""
+    for name in ("c1", "c2", "c3", "c5"):
+        assert _achromatic(scenes.CONFIGS[name].scene().to_abi()) == 1, name
+    assert _achromatic(scenes.CONFIGS["demo"].scene().to_abi()) == 0                 # red cube (MSA:588)
+    no_cube = scenes.load_scene([("b6", scenes.LIGHT), ("b4", scenes.TETRAHEDRON), ("d7", scenes.SPHERE)])
+    assert _achromatic(no_cube.to_abi()) == 1
+    sa = scenes.CONFIGS["c2"].scene().to_abi()
+    sa.lights[0].color[1] = 0.5                                                       # a tinted light
+    assert _achromatic(sa) == 0
+    sb = scenes.CONFIGS["c2"].scene().to_abi()
+    sb.white_square.diffuse[2] = 0.25                                                 # a tinted board square
+    assert _achromatic(sb) == 0
+    sb.has_board = 0                                                                  # ... unused without the board
+    assert _achromatic(sb) == 1
+    sc = scenes.CONFIGS["c2"].scene().to_abi()
+    sc.sphere_material.specular[0] = float("nan")                                     # NaN != NaN: not provably grey
+    assert _achromatic(sc) == 0
+
+
+def test_new_entry_points_fail_loudly_without_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    L = abi.lib()
+    p = ctypes.c_void_p()
+    assert L.rt_host_alloc(1024, ctypes.byref(p)) == abi.RT_EHIP
+    assert L.rt_render_packed(None, None, None, 16, 16, 1, abi.RT_PIXEL_GRAY8, None, None) == abi.RT_EINVAL
+    assert L.rt_ctx_wait(None, 0) == abi.RT_EINVAL
+    assert L.rt_group_timing(None, 1) == abi.RT_EINVAL

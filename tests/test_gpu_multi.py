@@ -252,6 +252,85 @@ def test_dropin_binding_demo_board(tmp_path):
     assert np.array_equal(_read_ppm(out), q)
 
 
+@pytest.mark.parametrize("opts", [["--format", "gray"], ["--pipelined"], ["--pageable", "--format", "rgba"],
+                                  ["--pipelined", "--pageable", "--format", "rgb"]])
+def test_dropin_binding_formats_and_pipelining(tmp_path, opts):
+    """The binding's frame formats (GRAY8 for the achromatic board: light, tetrahedron, spheres — no red cube),
+    pinned / pageable buffers and the pipelined draw() (the PPM is the last queued frame): the PPM equals the
+    oracle's frame, quantised, whatever crossed PCIe."""
+    exe = os.path.join(LIBDIR, "rt_dropin")
+    out = tmp_path / "dropin.ppm"
+    entries = ["b6:a", "b4:b", "d7:d", "f3:d"]
+    r = subprocess.run([exe, "--frames", "4", "--width", "320", "--height", "240", "--pitch", "1.5", "--out", str(out)]
+                       + opts + entries, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    if opts == ["--pipelined"]:
+        assert "GRAY8" in r.stdout and "pipelined" in r.stdout        # auto: achromatic board -> GRAY8
+    sc = scenes.load_scene([("b6", scenes.LIGHT), ("b4", scenes.TETRAHEDRON), ("d7", scenes.SPHERE),
+                            ("f3", scenes.SPHERE)])
+    want, _ = po.render(sc.to_abi(), scenes.make_camera(320, 240, 1.5), 320, 240, 5)
+    q = np.floor(np.clip(want, 0.0, 1.0) * 255.0 + 0.5).astype(np.uint8)[::-1]
+    assert np.array_equal(_read_ppm(out), q)
+
+
+def _devices():
+    return torch.cuda.device_count() if torch.cuda.is_available() else 0
+
+
+@pytest.mark.skipif(_devices() < 2, reason="needs >= 2 GPUs: the RCCL send/recv gather over distinct devices "
+                                           "(ncclCommInitAll) cannot run on a one-GPU box")
+@pytest.mark.parametrize("outputs", ["rgba8", "both"])
+def test_render_multi_rccl_distinct_devices(outputs):
+    """c4 over RCCL for real: one context per device (rt_group_create -> ncclCommInitAll), N = 2 ..
+    device_count ranks, 3840x2160 c3 frames with alternating eyes (double buffers in flight); rank 0's images
+    equal a one-launch render byte for byte, and the float64 one-launch frame hashes to the reference's c3."""
+    cfg = scenes.CONFIGS["c3"]
+    W, H = cfg.width, cfg.height
+    sc = cfg.scene()
+    one = Tracer(0)
+    one.set_scene(sc)
+    cams = [cfg.camera(), cfg.camera()]
+    cams[1].eye = abi.vec3((30.0, 140.0, 260.0))
+    want = []
+    for cam in cams:
+        b = one.render(cam, W, H, cfg.depth, rgba32f=True, rgba8=True, rgb64f=cam is cams[0])
+        torch.cuda.synchronize()
+        want.append(b)
+    assert f"{po.fnv1a64(want[0]['rgb64f'].cpu().numpy()):016x}" == golden.manifest()["frames"]["c3"]["fnv1a64"]
+    for n in sorted({2, min(4, _devices()), _devices()}):
+        ctxs = [Tracer(d) for d in range(n)]
+        for c in ctxs:
+            c.set_scene(sc)
+        g = _group(ctxs, abi.RT_TRANSPORT_RCCL)
+        try:
+            info = [ctypes.c_int() for _ in range(4)]
+            abi.check(abi.lib().rt_group_info(g, *[ctypes.byref(x) for x in info]), "rt_group_info")
+            assert [x.value for x in info] == [n, n, 0, abi.RT_TRANSPORT_RCCL]
+            abi.check(abi.lib().rt_group_timing(g, 1), "rt_group_timing")
+            with torch.cuda.device(0):
+                s = torch.cuda.Stream()
+                outs = [(torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0") if outputs == "both" else None,
+                         torch.empty((H, W, 4), dtype=torch.uint8, device="cuda:0")) for _ in range(6)]
+                for f in range(6):
+                    _multi(g, cams[f % 2], W, H, cfg.depth, 0, outs[f][0], outs[f][1], s)
+                s.synchronize()
+            abi.check(abi.lib().rt_group_synchronize(g), "rt_group_synchronize")
+            for f in range(6):
+                assert torch.equal(outs[f][1], want[f % 2]["rgba8"]), (n, f)
+                if outputs == "both":
+                    assert torch.equal(outs[f][0], want[f % 2]["rgba32f"]), (n, f)
+            st = abi.rt_group_stats()
+            abi.check(abi.lib().rt_group_get_stats(g, ctypes.byref(st)), "rt_group_get_stats")
+            assert st.wire_byte == abi.RT_PIXEL_GRAY8 and st.ranks_timed == n and st.gather_ms > 0
+            print(f"n={n}: render {st.render_ms:.3f} ms, gather {st.gather_ms:.3f} ms, assemble "
+                  f"{st.assemble_ms:.3f} ms, frame {st.frame_ms:.3f} ms, payload {st.payload_bytes} B")
+        finally:
+            abi.lib().rt_group_destroy(g)
+            for c in ctxs:
+                c.close()
+    one.close()
+
+
 def test_dropin_rejects_cylinder(tmp_path):
     exe = os.path.join(LIBDIR, "rt_dropin")
     r = subprocess.run([exe, "--out", str(tmp_path / "x.ppm"), "b6:a", "c3:e"], capture_output=True, text=True,

@@ -6,9 +6,10 @@ set -eu
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 SRC=$ROOT/ray_tracer_fragment_shader_amd/csrc
 out=$(mktemp -d)
-( cd "$SRC" && /opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -fno-fast-math -Wno-unused-function \
-    --offload-arch=gfx950 --cuda-device-only -S -DRT_MAX_B=${RT_MAX_B:-3} "$@" rt_kernel.hip -o "$out/k.s" \
-    -Rpass-analysis=kernel-resource-usage 2> "$out/ru.txt" )
+( cd "$SRC" && for b in $(seq 0 ${RT_MAX_B:-3}); do
+    /opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -fno-fast-math -Wno-unused-function \
+    --offload-arch=gfx950 --cuda-device-only -S "$@" rt_render_b$b.hip -o "$out/k$b.s" \
+    -Rpass-analysis=kernel-resource-usage 2> "$out/ru$b.txt" & done; wait; cat "$out"/ru*.txt > "$out/ru.txt" )
 python3 - "$out/ru.txt" <<'EOF'
 import re, sys
 cur = None
