@@ -75,6 +75,10 @@
 #ifndef RT_HITS_INSIDE
 #define RT_HITS_INSIDE 1
 #endif
+// 1: the bounce loop of trace() is unrolled (one copy of the level code per level); 0: a loop (one copy).
+#ifndef RT_UNROLL_LEVELS
+#define RT_UNROLL_LEVELS 1
+#endif
 // A/B only: 0 reads the per-eye flag from the scene header at each use (wrong for ray lists)
 #ifndef RT_HITS_VIEW
 #define RT_HITS_VIEW 1
@@ -95,7 +99,18 @@
 #define RT_SKIP_FAST_MIN_B 2
 #endif
 
+// 1: diagnostic build (tools/counters.py): wave-level event counters in DevScene::counters.
+#ifndef RT_COUNTERS
+#define RT_COUNTERS 0
+#endif
+
 namespace rt {
+
+// Counter slots of RT_COUNTERS builds.
+enum Counter {
+    kCntWaves = 0, kCntConeKept, kCntRayMasks, kCntRayKept, kCntShadowMasks, kCntShadowKept, kCntExactRay,
+    kCntExactShadow, kCntBoardShadow, kCntLevels, kCntExactPrimary, kCntFilterRay, kCntFilterShadow, kCntCount
+};
 
 struct d3 {
     double x, y, z;
@@ -243,6 +258,13 @@ __device__ __forceinline__ d3 unit(d3 a) {
 // LDS in the render kernel (or in global memory for the ray-list kernels); the FP32 filter images `sphf`,
 // `primf` are always read from global memory with wave-uniform indices, i.e. through the scalar cache
 // into SGPR operands.
+// One count per wave (from its first active lane) in RT_COUNTERS builds.
+#define RT_COUNT(S, slot, v)                                                                                   \
+    do {                                                                                                       \
+        if (RT_COUNTERS && (S)->counters && __lane_id() == __builtin_ctzll(__ballot(1)))                       \
+            atomicAdd((S)->counters + (slot), (unsigned long long)(v));                                        \
+    } while (0)
+
 struct SceneView {
     const DevScene* S;
     const DevSphere* sph;
@@ -594,7 +616,9 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
     if (CULL && V.np >= kConeMin) {
         for (uint64_t m = mask & sphere_bits(V.np); m; m &= m - 1) {
             const int k = __builtin_ctzll(m);
+            RT_COUNT(S, kCntFilterRay, 1);
             if (k == skip - 1 || sphere_reject32(V.sphf[k], r)) continue;
+            RT_COUNT(S, kCntExactRay, 1);
             d3 q;
             if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) {
                 double dist = len_fast(sub(q, r.p0));       // :811-812
@@ -626,6 +650,7 @@ __device__ __forceinline__ void primary_sphere(const SceneView& V, const Ray& r,
     if (fmaf(uD, uD, f.c0) < 0.0f) return;                  // certain disc < 0
     const DevSpherePrim& pp = V.prim[k];
     d3 q;
+    RT_COUNT(V.S, kCntExactPrimary, 1);
     if (sphere_hit_dp(ld3(pp.dP), pp.dd, V.sph[k].r2, r.p0, r.u, eps, &q)) {
         double dist = len_fast(sub(q, r.p0));
         if (dist < *best || *best < 0.0) {
@@ -657,7 +682,7 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
     }
     const double eps = S->eps;
     int k0 = 0;
-    if (V.np >= kConeMin) {
+    if (V.np >= kPrimaryConeMin) {
         for (uint64_t m = cone & sphere_bits(V.np); m; m &= m - 1)
             primary_sphere(V, r, __builtin_ctzll(m), eps, &kind, &best, hp);
         k0 = 64;
@@ -706,6 +731,40 @@ __device__ __host__ __forceinline__ float chord_of_sin(float s) {
     return s * sqrtf(2.0f / (1.0f + sqrtf(fmaxf(0.0f, 1.0f - s * s))));
 }
 
+// FP32 square root and reciprocal of the wave-culling tests (RT_FAST_MASK = 1): the hardware instructions
+// (v_sqrt_f32, v_rcp_f32, 1 ulp: relative error < 2^-22 on normal operands) instead of the correctly rounded
+// sequences (scaling, Newton and fixup steps around them: ~10 instructions each).  The culling tests only need
+// conservative bounds, and their margins (R inflated by 2^-12 relative, chord limits by 2^-14 absolute, shadow
+// cones by 2^-16 in cos) are > 2^6 times the extra error; 0, +inf and NaN keep their meaning (sqrt(0) = 0,
+// rcp(+inf) = 0, NaN propagates and fails the `>` compares, i.e. keeps the sphere).
+#ifndef RT_FAST_MASK
+#define RT_FAST_MASK 1                         // same-box A/B: c5 -5.7%, c2/c3 +-1%
+#endif
+__device__ __forceinline__ float msqrt(float x) {
+#if RT_FAST_MASK
+    return __builtin_amdgcn_sqrtf(x);
+#else
+    return sqrtf(x);
+#endif
+}
+__device__ __forceinline__ float mrcp(float x) {
+#if RT_FAST_MASK
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+__device__ __forceinline__ float mdiv(float a, float b) {
+#if RT_FAST_MASK
+    return a * __builtin_amdgcn_rcpf(b);
+#else
+    return a / b;
+#endif
+}
+__device__ __forceinline__ float mchord_of_sin(float s) {
+    return s * msqrt(mdiv(2.0f, 1.0f + msqrt(fmaxf(0.0f, 1.0f - s * s))));
+}
+
 // Per-wave culling of primary rays (V.np >= kConeMin; all 64 lanes must be active).  The wave's rays go
 // from the eye through the screen points of its bw x bh block, all within R = half_diag pitch of the
 // block centre c (half_diag = |((bw - 1) / 2, (bh - 1) / 2)|), hence (exact geometry) within angle asin(R / |c - eye|) of a = unit(c - eye): chord
@@ -721,11 +780,12 @@ __device__ __forceinline__ uint64_t primary_cone_mask(const SceneView& V, const 
     float dx = fmaf(a_u, upp[0], fmaf(a_r, right[0], look[0])) - eye[0];
     float dy = fmaf(a_u, upp[1], fmaf(a_r, right[1], look[1])) - eye[1];
     float dz = fmaf(a_u, upp[2], fmaf(a_r, right[2], look[2])) - eye[2];
-    const float dn = sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz)));
-    const float sn = (half_diag * 1.001f) * pitch / dn;
+    const float dn = msqrt(fmaf(dx, dx, fmaf(dy, dy, dz * dz)));
+    const float sn = mdiv((half_diag * 1.001f) * pitch, dn);
     if (!(sn < 0.5f)) return ~0ull;                         // eye too close to the screen: no culling
-    const float rho = chord_of_sin(sn) + slack;
-    dx /= dn, dy /= dn, dz /= dn;
+    const float rho = mchord_of_sin(sn) + slack;
+    const float idn = mrcp(dn);
+    dx *= idn, dy *= idn, dz *= idn;
     bool keep = false;
     if (lane < V.np) {
         const DevSphereCone& c = V.cone[lane];
@@ -787,29 +847,33 @@ __device__ __forceinline__ uint64_t ray_bundle_mask(const SceneView& V, bool on,
         dp = inf_if_nan(fmaf(px, px, fmaf(py, py, pz * pz)));
         du = inf_if_nan(fmaf(ux, ux, fmaf(uy, uy, uz * uz)));
     }
-    const float rho_o = sqrtf(wave_max(dp)), rho_d = sqrtf(wave_max(du));
+    const float rho_o = msqrt(wave_max(dp)), rho_d = msqrt(wave_max(du));
     if (!(rho_d < 1.0f) || !(rho_o < 1e30f)) return ~0ull;   // spread too wide: no culling
     bool keep = false;
     if (lane < V.np) {
         const DevSphereF& c = V.sphf[lane];
         if (c.rm >= 0.0f) {                                   // padding spheres: rm = -inf
             const float vx = c.cx - ox, vy = c.cy - oy, vz = c.cz - oz;
-            const float D = sqrtf(fmaf(vx, vx, fmaf(vy, vy, vz * vz)));
+            const float D = msqrt(fmaf(vx, vx, fmaf(vy, vy, vz * vz)));
             const float Dm = D + rho_o;
             const float scale = fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz))) +
                                 fmaxf(fabsf(c.cx), fmaxf(fabsf(c.cy), fabsf(c.cz))) + 1.0f;
-            const float R = (sqrtf(fmaf(c.rm, 1.0f + 0x1p-20f, Dm * Dm * 0x1p-46f)) + rho_o) * (1.0f + 0x1p-12f) +
+            const float R = (msqrt(fmaf(c.rm, 1.0f + 0x1p-20f, Dm * Dm * 0x1p-46f)) + rho_o) * (1.0f + 0x1p-12f) +
                             0x1p-12f * scale;
             if (!(D > R)) {
                 keep = true;
             } else {
-                const float lim = rho_d + chord_of_sin(R / D) + 0x1p-14f;
-                const float ex = ax - vx / D, ey = ay - vy / D, ez = az - vz / D;
+                const float iD = mrcp(D);
+                const float lim = rho_d + mchord_of_sin(R * iD) + 0x1p-14f;
+                const float ex = ax - vx * iD, ey = ay - vy * iD, ez = az - vz * iD;
                 keep = !(fmaf(ex, ex, fmaf(ey, ey, ez * ez)) > lim * lim);
             }
         }
     }
-    return __ballot(keep);
+    const uint64_t kept = __ballot(keep);
+    RT_COUNT(V.S, kCntRayMasks, 1);
+    RT_COUNT(V.S, kCntRayKept, __popcll(kept & sphere_bits(V.np)));
+    return kept;
 }
 
 // Shadow rays to light li: every ray lies on a line through the light, with direction w_l = u_l.
@@ -827,20 +891,23 @@ __device__ __forceinline__ uint64_t shadow_bundle_mask(const SceneView& V, bool 
         const float ux = r.ux - ax, uy = r.uy - ay, uz = r.uz - az;
         du = inf_if_nan(fmaf(ux, ux, fmaf(uy, uy, uz * uz)));      // squared (see ray_bundle_mask)
     }
-    const float rho = sqrtf(wave_max(du));
+    const float rho = msqrt(wave_max(du));
     if (!(rho < 1.0f)) return ~0ull;
     bool keep = false;
     if (lane < V.np) {
         const DevSphereLightF& c = V.lightf[li * V.np + lane];
         if (c.c <= 1.0f) {
-            const float lim = rho + sqrtf(fmaxf(0.0f, 2.0f - 2.0f * c.c)) + 0x1p-14f;
+            const float lim = rho + msqrt(fmaxf(0.0f, 2.0f - 2.0f * c.c)) + 0x1p-14f;
             const float l2 = lim * lim;
             const float ex = ax - c.vx, ey = ay - c.vy, ez = az - c.vz;
             const float fx = ax + c.vx, fy = ay + c.vy, fz = az + c.vz;
             keep = !(fmaf(ex, ex, fmaf(ey, ey, ez * ez)) > l2) || !(fmaf(fx, fx, fmaf(fy, fy, fz * fz)) > l2);
         }
     }
-    return __ballot(keep);
+    const uint64_t kept = __ballot(keep);
+    RT_COUNT(V.S, kCntShadowMasks, 1);
+    RT_COUNT(V.S, kCntShadowKept, __popcll(kept & sphere_bits(V.np)));
+    return kept;
 }
 
 // Shadow test: intersects() of g_scene.intersection(Line(pt, Lpos)) (:1216-1221), any hit.
@@ -865,7 +932,9 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
             float t = r.ux * f.vx;
             t = fmaf(r.uy, f.vy, t);
             t = fmaf(r.uz, f.vz, t);
+            RT_COUNT(S, kCntFilterShadow, 1);
             if (fabsf(t) < f.c || k == skip - 1) continue;
+            RT_COUNT(S, kCntExactShadow, 1);
             d3 q;
             if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) return true;
         }
@@ -898,6 +967,7 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
     }
     if (S->has_board && skip != 0) {
         d3 q;
+        RT_COUNT(S, kCntBoardShadow, 1);
         if (board_hit(S, r.p0, r.d, &q)) return true;
     }
     for (int m = 0; FULL && m < V.nm; ++m) {
@@ -1060,6 +1130,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
                                            uint64_t cone, Ray* r, int* levels, uint32_t* nseg, uint32_t* nsh,
                                            double* slot, int* mslot, int* skip) {
     uint64_t smask = ~0ull;
+    RT_COUNT(V.S, kCntLevels, 1);
     if (!first) {
         set_origin_f32(V.S, r);
         if (V.np >= kConeMin) smask = ray_bundle_mask(V, alive, *r);
@@ -1132,7 +1203,11 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
     int skip = -1;                                          // origin_skip of r's origin
     constexpr bool kSkip = !TRANSP && B >= RT_SKIP_FAST_MIN_B;  // fast loop: origin skips from this depth
     constexpr bool kPark = B >= RT_PARK_ND_MIN_B;
+#if RT_UNROLL_LEVELS
 #pragma unroll
+#else
+#pragma unroll 1
+#endif
     for (int lvl = 0; lvl <= B; ++lvl) {
         const bool alive = lvl == 0 || levels == lvl;
         if (!__any(alive)) break;                           // the whole wave has missed: early out

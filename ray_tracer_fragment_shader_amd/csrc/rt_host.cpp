@@ -411,6 +411,7 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     d->tree = tree ? 1 : 0;
     d->hits_inside = 0;                  // set below, once every object's extent is known
     d->hits_lim2 = -1.0;
+    d->counters = nullptr;
     d->hits_ok = 0;                      // per eye, rt_prepare_kernel
     d->n_lights = s->n_lights;
     for (int k = 0; k < s->n_lights; ++k) {

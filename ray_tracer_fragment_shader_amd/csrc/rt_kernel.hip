@@ -407,6 +407,17 @@ extern "C" int rt_debug_wave_trace(void* dev_buf) {
 }
 #endif
 
+#if RT_COUNTERS
+// Diagnostic build only (tools/counters.py): point the uploaded scene's event counters at `dev_buf`
+// (kCntCount uint64 on the context's device); call after rt_set_scene.
+extern "C" int rt_debug_counters(rt_ctx* c, void* dev_buf) {
+    if (!c || !c->scene_set) return rt_fail(RT_EINVAL, "rt_debug_counters: no scene");
+    RT_HIP(hipSetDevice(c->device));
+    RT_HIP(hipMemcpy(&c->d_scene->counters, &dev_buf, sizeof(dev_buf), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+#endif
+
 extern "C" int rt_device_count(int* count) {
     if (!count) return rt_fail(RT_EINVAL, "rt_device_count: null pointer");
     int n = 0;

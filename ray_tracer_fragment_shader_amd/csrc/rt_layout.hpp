@@ -25,6 +25,12 @@ constexpr int kChunk = 4;              // spheres per branch-free filter batch
 #define RT_CONE_MIN 16
 #endif
 constexpr int kConeMin = RT_CONE_MIN;   // per-wave culling (primary cones, ray and shadow bundles) from this many (padded) spheres
+// The primary-ray cone mask is one ballot per wave (fast FP32 math): from 8 spheres it beats the per-sphere
+// FP32 filter batches it replaces (same-box A/B: c2 -0.8%, c3 -1.9%; from 4 spheres c1 +3.7%).
+#ifndef RT_PRIMARY_CONE_MIN
+#define RT_PRIMARY_CONE_MIN 8
+#endif
+constexpr int kPrimaryConeMin = RT_PRIMARY_CONE_MIN;   // the primary-ray cone mask alone (every kernel variant)
 
 // FP32 filter margin factor: 256 unit roundoffs of binary32.  The filter's own error is below
 // 64 * 2^-24 * (S^2 + r^2) (error budget in rt_device.hpp, sphere_reject32), so a margin of
@@ -125,6 +131,7 @@ struct alignas(16) DevScene {
     int32_t tree;                      // some material transmits AND reflects: ray-tree kernels (trace_tree)
     int32_t hits_inside;               // every hit point lies within (R - 1) of bc: rays from hits pass the cull
     int32_t hits_ok;                   // hits_inside for the camera eye (rt_prepare_kernel, per eye)
+    unsigned long long* counters;      // RT_COUNTERS builds (tools/counters.py): per-wave event counters, else null
     DevTri tri[2];                     // board triangles T1 = (P1,P2,P3), T2 = (P1,P3,P4)   (:840-841)
     DevMat mat[5];                     // 0 white square, 1 black square, 2 sphere, 3 tetrahedron, 4 cube
     DevLight light[16];

@@ -164,13 +164,14 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
                                                              RenderParams P, void* __restrict__ out32,
                                                              void* __restrict__ out8,
                                                              double* __restrict__ out64,
-                                                             uint32_t* __restrict__ outrc) {
+                                                             uint32_t* __restrict__ outrc,
+                                                             const int32_t* __restrict__ tile_rows) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
 #if RT_WAVE_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    const uint64_t t_cal = P.row_cost ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t t_cal = __builtin_amdgcn_s_memrealtime();   // used by calibration renders (P.row_cost)
     // LDS: [header | DevSphere[np] | DevSpherePrim[np]] (LDS = 1), the per-level colour slots of trace()
     // (slot_bytes), then the output staging tile (12 KB, RT_WG_STAGING only).
     // The scene record is broadcast into LDS once per workgroup; the FP32 filter images stay in global
@@ -203,15 +204,21 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
     const int cy = lane >> 3;                      // row inside the tile
     const int tx = blockIdx.x;                      // 2-D grid: tiles_x x tiles_y
     const int gy = (int)(blockIdx.z * kGridY + blockIdx.y);    // tile rows beyond kGridY go to grid.z
-    const int ty = P.tile_rows ? P.tile_rows[gy] : gy;
-    if ((unsigned)ty >= (unsigned)P.tile_rows_n) return;        // padding of the last grid.z slice
+    // (a const __restrict__ kernel argument: a scalar load, issued beside the other argument loads; through
+    // RenderParams it was a vector load the whole prologue waited for)
+    // Padding tiles of the last grid.z slice trace a clamped tile and store nothing (no early return: a branch
+    // here kept the compiler from issuing the scene loads until the tile row had arrived).
+    const int ty_raw = tile_rows ? tile_rows[gy] : gy;
+    const bool pad = (unsigned)ty_raw >= (unsigned)P.tile_rows_n;
+    const int ty = pad ? P.tile_rows_n - 1 : ty_raw;
     const int i = tx * TW + cx;
     const int lr = ty * kTileH + cy;
-    const bool valid = i < P.width && lr < P.local_rows;
+    const bool valid = i < P.width && lr < P.local_rows && !pad;
 
     // Per-wave sphere culling (all lanes active here).  The block's rows must be contiguous image rows.
     uint64_t cone = ~0ull;
-    if (P.np >= kConeMin) {
+    RT_COUNT(V.S, kCntWaves, 1);
+    if (P.np >= kPrimaryConeMin) {
         // Within one frame global_row_of is increasing, so jb - ja == 7 means 8 consecutive rows.
         const int lr0 = ty * kTileH + by0, ja = global_row_of(P, lr0), jb = global_row_of(P, lr0 + bh - 1);
         const bool one_frame = P.frames <= 1 || lr0 / P.frame_rows == (lr0 + bh - 1) / P.frame_rows;
@@ -220,6 +227,7 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
             cone = primary_cone_mask(V, P.look32, P.right32, P.upp32, P.eye32, P.pitch32,
                                      (float)(tx * TW + bx0 + P.bottom_x) + hx, (float)(ja + P.bottom_y) + hy,
                                      sqrtf(hx * hx + hy * hy), P.cone_slack, lane);
+        RT_COUNT(V.S, kCntConeKept, __popcll(cone & sphere_bits(V.np)));
     }
 
     // Every lane traces (trace() reduces over the wave): lanes outside the frame trace a clamped pixel
@@ -247,7 +255,7 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
             if (out64) { out64[3 * k] = col.x; out64[3 * k + 1] = col.y; out64[3 * k + 2] = col.z; }
             if (outrc) outrc[k] = seg | (sh << 16);
         }
-        if (P.row_cost && tid == 0)
+        if (P.row_cost && tid == 0 && !pad)
             atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
 #if RT_WAVE_TRACE
         if (P.wtrace && tid == 0) {
@@ -270,7 +278,7 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
     __syncthreads();
     const int oy = tid >> 5, ox = tid & 31;
     const int gi = tx * kTileW + ox, glr = ty * kTileH + oy;
-    if (gi < P.width && glr < P.local_rows) {
+    if (gi < P.width && glr < P.local_rows && !pad) {
         const size_t k = (size_t)glr * P.width + gi;
         if (out32) reinterpret_cast<float4*>(out32)[k] = st32[tid];
         if (out64) {
@@ -281,7 +289,7 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
         if (outrc) outrc[k] = strc[tid];
         if (out8) reinterpret_cast<uchar4*>(out8)[k] = st8[tid];
     }
-    if (P.row_cost && tid == 0) atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
+    if (P.row_cost && tid == 0 && !pad) atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
 }
 
 // rayTraceRay on a list of rays Line(starts[k], ends[k]).  Rays from arbitrary starts: whether their hit
@@ -373,7 +381,8 @@ hipError_t launch_render_one(const RenderLaunch& L) {
         hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, L.grid, dim3(WG), L.lds, L.stream, L.scene, L.P, L.o32, L.o8, L.o64, L.orc);
+    hipLaunchKernelGGL(kern, L.grid, dim3(WG), L.lds, L.stream, L.scene, L.P, L.o32, L.o8, L.o64, L.orc,
+                       L.P.tile_rows);
     return hipGetLastError();
 }
 
