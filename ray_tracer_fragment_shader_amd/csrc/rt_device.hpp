@@ -203,15 +203,39 @@ __device__ __forceinline__ double div_const(double a, double b, double r, int32_
 #endif
 }
 
+// The compiler's IEEE sqrt sequence on gfx950, restated op for op (same bits for every input): x below 2^-767
+// is scaled by 2^256, sqrt_core, the result scaled by 2^-128, and +-0 / +inf return the (scaled) input.  Its
+// constants (256, -128, the class mask) come from opaque SGPR moves: the compiler's own expansion hoisted them
+// out of the bounce loop into three VGPRs held across the whole kernel for this rarely taken path, which cost
+// the register headroom of a seventh wave per SIMD at c2.
+// RT_SQRT_IEEE_ASM=0 (experiment builds): the compiler's sqrt() instead; the c5 culling kernel then needs
+// 83 VGPRs (5 waves per SIMD) and runs +6% (same-box A/B).
+#ifndef RT_SQRT_IEEE_ASM
+#define RT_SQRT_IEEE_ASM 1
+#endif
+__device__ __forceinline__ double sqrt_ieee(double x) {
+#if !RT_SQRT_IEEE_ASM
+    return sqrt(x);
+#endif
+    int up, down, cls;
+    asm volatile("s_mov_b32 %0, 0x100" : "=s"(up));
+    asm volatile("s_mov_b32 %0, 0xffffff80" : "=s"(down));
+    asm volatile("s_mov_b32 %0, 0x260" : "=s"(cls));          // class: -0, +0, +inf
+    const bool small = x < 0x1p-767;
+    const double xs = __builtin_amdgcn_ldexp(x, small ? up : 0);
+    const double g = __builtin_amdgcn_ldexp(sqrt_core(xs), small ? down : 0);
+    return __builtin_amdgcn_class(xs, cls) ? xs : g;
+}
+
 // sqrt(x), bit-identical, with the fast sequence when it applies.
 __device__ __forceinline__ double sqrt_fast(double x) {
 #if RT_FAST_FALLBACK
     const bool ok = sqrt_fast_ok(x);
     double y = sqrt_core(x);
-    if (any_lane(!ok)) y = ok ? y : sqrt(x);
+    if (any_lane(!ok)) y = ok ? y : sqrt_ieee(x);
     return y;
 #else
-    return sqrt_fast_ok(x) ? sqrt_core(x) : sqrt(x);
+    return sqrt_fast_ok(x) ? sqrt_core(x) : sqrt_ieee(x);
 #endif
 }
 
@@ -229,7 +253,7 @@ __device__ __forceinline__ d3 unit(d3 a, double* l) {
               copysign(div_core(a.z, L, r), a.z));
     if (any_lane(!ok)) {
         if (!ok) {
-            L = sqrt(s);
+            L = sqrt_ieee(s);
             u = divs(a, L);
         }
     }
@@ -243,7 +267,7 @@ __device__ __forceinline__ d3 unit(d3 a, double* l) {
         return mk(copysign(div_core(a.x, L, r), a.x), copysign(div_core(a.y, L, r), a.y),
                   copysign(div_core(a.z, L, r), a.z));
     }
-    double L = sqrt(s);
+    double L = sqrt_ieee(s);
     *l = L;
     return divs(a, L);
 #endif
@@ -831,11 +855,8 @@ __device__ __forceinline__ float inf_if_nan(float v) { return v >= 0.0f ? v : __
 // and v = unit(C_k - o) is at most asin(R / |C_k - o|), i.e. |a - v| <= rho_d + chord(R / |C_k - o|).
 // FP32 coordinates carry < 2^-20 relative error; R gets 2^-12 (|o| + |C| + 1) absolute and the chord
 // test 2^-14 of slack.
-__device__ __forceinline__ uint64_t ray_bundle_mask(const SceneView& V, bool on, const Ray& r) {
+__device__ __forceinline__ uint64_t ray_bundle_part(const SceneView& V, bool on, const Ray& r, int f) {
     const int lane = __lane_id();
-    const uint64_t onm = __ballot(on);
-    if (!onm) return 0;
-    const int f = __builtin_ctzll(onm);
     const float ox = lane_f32(r.px, f), oy = lane_f32(r.py, f), oz = lane_f32(r.pz, f);
     const float ax = lane_f32(r.ux, f), ay = lane_f32(r.uy, f), az = lane_f32(r.uz, f);
     // squared spreads reduced, one square root on the maxima (sqrt is monotonic: the same rho as the max
@@ -874,6 +895,31 @@ __device__ __forceinline__ uint64_t ray_bundle_mask(const SceneView& V, bool on,
     RT_COUNT(V.S, kCntRayMasks, 1);
     RT_COUNT(V.S, kCntRayKept, __popcll(kept & sphere_bits(V.np)));
     return kept;
+}
+
+// 1: a wave whose rays fan out (a sphere's silhouette: mirror rays off the board beside grazing reflections
+// off the sphere) is covered by two bundles — the lanes within chord 0.9 of the first lane's direction (always
+// narrow enough to cull) and the rest — and the mask is their union (each part is conservative for its lanes);
+// 0: one bundle, no culling once the directions spread past chord 1.
+#ifndef RT_BUNDLE_SPLIT
+#define RT_BUNDLE_SPLIT 1
+#endif
+__device__ __forceinline__ uint64_t ray_bundle_mask(const SceneView& V, bool on, const Ray& r) {
+    const uint64_t onm = __ballot(on);
+    if (!onm) return 0;
+    const int f = __builtin_ctzll(onm);
+#if RT_BUNDLE_SPLIT
+    const float ax = lane_f32(r.ux, f), ay = lane_f32(r.uy, f), az = lane_f32(r.uz, f);
+    const float ux = r.ux - ax, uy = r.uy - ay, uz = r.uz - az;
+    const bool near = on && fmaf(ux, ux, fmaf(uy, uy, uz * uz)) < 0.81f;     // NaN: not near
+    uint64_t m = ray_bundle_part(V, near, r, f);
+    const bool rest = on && !near;
+    const uint64_t restm = __ballot(rest);
+    if (restm) m |= ray_bundle_part(V, rest, r, __builtin_ctzll(restm));
+    return m;
+#else
+    return ray_bundle_part(V, on, r, f);
+#endif
 }
 
 // Shadow rays to light li: every ray lies on a line through the light, with direction w_l = u_l.
@@ -1014,7 +1060,7 @@ __device__ __forceinline__ d3 transmitted_end(const SceneView& V, int kind, int 
     double cti = dot(u, n);                                 // :690
     double modulus = 1 - rr * rr * (1 - cti * cti);         // :691
     if (modulus > 0) {
-        double ctr = sqrt(modulus);
+        double ctr = sqrt_ieee(modulus);
         t = sub(scl(rr, u), scl(ctr + rr * cti, n));        // :696
     }
     return add(p, t);                                       // Line(p, p + t) (:699)
@@ -1042,11 +1088,18 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
 // direction, rdir = reflectedRay().direction() (:1225).  `hit` marks the lanes whose colour is wanted.  CULL: called by all
 // lanes of the wave, the light loop stays converged for shadow_bundle_mask; otherwise only by hit lanes.
 // FULL: meshes may be present and materials may be transparent (closest-hit shadows, :1219-1221).
-template <bool FULL, bool CULL>
+// ACC: the colour is accumulated in LDS at acc[0], acc[SS], acc[2 SS] (starting at 0, the same additions in the
+// same order) instead of in registers live across every light's shadow test; the return value is then unused.
+template <bool FULL, bool CULL, bool ACC = false, int SS = 256>
 __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, int mat, double ks,
-                                    int skip = -1) {
+                                    int skip = -1, double* acc = nullptr) {
     const DevScene* S = V.S;
     d3 color = mk(0.0, 0.0, 0.0);
+    if (ACC) {
+        acc[0] = 0.0;
+        acc[SS] = 0.0;
+        acc[2 * SS] = 0.0;
+    }
     Ray sr;
     sr.p0 = p;
     if (FULL) set_origin_f32(S, &sr);                       // closest-hit shadows use the ray filter
@@ -1066,11 +1119,27 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
             double a = S->att / (S->att + dl * dl);         // attenuation (:1181)
             d3 lC = scl(a, ld3(S->light[i].col));           // :1223
             d3 term = add(add(had(ld3(M.amb), lC), scl(kd, had(ld3(M.diff), lC))), scl(ks, had(ld3(M.spec), lC)));
-            color = add(color, term);                       // :1224-1226
+            if (ACC) {                                      // :1224-1226, in LDS
+                acc[0] = acc[0] + term.x;
+                acc[SS] = acc[SS] + term.y;
+                acc[2 * SS] = acc[2 * SS] + term.z;
+            } else {
+                color = add(color, term);                   // :1224-1226
+            }
         }
     }
     return color;
 }
+
+// The fast loop (non-CULL, opaque) at depth 1 accumulates each level's colour in its LDS slot (shade ACC), which
+// frees the 6 VGPRs the colour held across the light loop (c2: 7 waves per SIMD without spills); the continuation
+// parked across that loop then needs one extra slot (slot B + 1).  Deeper kernels keep the colour in registers:
+// the extra slot would cost them LDS occupancy (B = 2 at 7 waves: 172 KB per CU).
+#ifndef RT_ACC_LDS_MAX_B
+#define RT_ACC_LDS_MAX_B 1
+#endif
+__host__ __device__ constexpr bool acc_lds(int B, bool transp) { return !transp && B >= 1 && B <= RT_ACC_LDS_MAX_B; }
+__host__ __device__ constexpr int colour_slots(int B, bool transp) { return B + 1 + (acc_lds(B, transp) ? 1 : 0); }
 
 // rayTraceRay(g_scene, lights, Line(p0, p1), color, B) with color starting at 0 (:1184-1249), as a loop.
 // Every hit of a non-tree scene spawns exactly one continuation (host-checked; ray trees: trace_tree): the
@@ -1127,7 +1196,7 @@ __device__ __forceinline__ void next_ray(d3 p, d3 nd, d3 nu, Ray* r) {
 // shadow_bundle_mask reduce over it).  Returns false when no lane hit (the bounce loop ends).
 template <int B, bool TRANSP, int SS = kSlotStride>
 __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool first, bool alive, d3 bdP, double bdd,
-                                           uint64_t cone, Ray* r, int* levels, uint32_t* nseg, uint32_t* nsh,
+                                           uint64_t cone, Ray* r, int* levels,
                                            double* slot, int* mslot, int* skip) {
     uint64_t smask = ~0ull;
     RT_COUNT(V.S, kCntLevels, 1);
@@ -1138,7 +1207,6 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     d3 p = mk(0.0, 0.0, 0.0);
     int kind = -1;
     if (alive) {
-        ++*nseg;
         kind = first ? closest_hit_primary<TRANSP>(V, *r, bdP, bdd, cone, &p)
                      : closest_hit<TRANSP, true>(V, *r, &p, smask, TRANSP ? -1 : *skip, lvl > 0);
     }
@@ -1180,7 +1248,6 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
             nu = mk(psl[3 * SS], psl[4 * SS], psl[5 * SS]);
         }
         park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
-        *nsh += V.nl;
         *levels = lvl + 1;
     }
     if (lvl < B) {
@@ -1199,7 +1266,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
     r.p0 = p0;
     d3 d = sub(p1, p0);
     set_dir(&r, d, unit(d));
-    uint32_t nseg = 0, nsh = 0;
+    // rays traced (seg, shadow) follow from `levels`: every lane traces levels 0 .. min(levels, B), nl shadow rays per hit
     int skip = -1;                                          // origin_skip of r's origin
     constexpr bool kSkip = !TRANSP && B >= RT_SKIP_FAST_MIN_B;  // fast loop: origin skips from this depth
     constexpr bool kPark = B >= RT_PARK_ND_MIN_B;
@@ -1213,14 +1280,13 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
         if (!__any(alive)) break;                           // the whole wave has missed: early out
         const bool first = PRIMARY && lvl == 0;
         if (CULL) {
-            if (!cull_level<B, TRANSP, SS>(V, lvl, first, alive, bdP, bdd, cone, &r, &levels, &nseg, &nsh, slot, mslot,
+            if (!cull_level<B, TRANSP, SS>(V, lvl, first, alive, bdP, bdd, cone, &r, &levels, slot, mslot,
                                            &skip))
                 break;
         } else {
             d3 p = mk(0.0, 0.0, 0.0);
             int kind = -1;
             if (alive) {
-                ++nseg;
                 if (first) {
                     kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p);
                 } else {
@@ -1257,22 +1323,24 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
                     nsl[2 * SS] = nu.z;
                 }
 #endif
+                // with the colour accumulated in this level's slot (kAcc), the end - start waits in slot lvl + 2
+                constexpr bool kAcc = acc_lds(B, TRANSP);
+                double* ndsl = kAcc ? psl + 6 * SS : psl;
                 if ((kPark || RT_PARK_NU) && lvl < B) {
-                    psl[0] = nd.x;
-                    psl[SS] = nd.y;
-                    psl[2 * SS] = nd.z;
+                    ndsl[0] = nd.x;
+                    ndsl[SS] = nd.y;
+                    ndsl[2 * SS] = nd.z;
                     asm volatile("" ::: "memory");          // keep it in LDS across the light loop
                 }
-                const d3 c = shade<TRANSP, false>(V, true, p, n, mat, ks, skip);
+                const d3 c = shade<TRANSP, false, kAcc, SS>(V, true, p, n, mat, ks, skip, psl);
                 if ((kPark || RT_PARK_NU) && lvl < B) {
                     asm volatile("" ::: "memory");
-                    nd = mk(psl[0], psl[SS], psl[2 * SS]);
+                    nd = mk(ndsl[0], ndsl[SS], ndsl[2 * SS]);
 #if RT_PARK_NU
                     nu = mk(psl[3 * SS], psl[4 * SS], psl[5 * SS]);
 #endif
                 }
-                park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
-                nsh += V.nl;
+                if (!kAcc) park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
                 levels = lvl + 1;
             }
 #if RT_KEEP_NU || RT_PARK_NU
@@ -1290,8 +1358,8 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
         if (lvl == levels - 1) acc = c;
         else acc = TRANSP ? add(c, had(ld3(S->mat[mslot[lvl * SS]].w), acc)) : add(c, acc);
     }
-    *seg = nseg;
-    *shadow = nsh;
+    *seg = (uint32_t)(levels < B + 1 ? levels + 1 : B + 1);
+    *shadow = (uint32_t)(V.nl * levels);
     return acc;
 }
 

@@ -41,9 +41,19 @@
 #ifndef RT_WG_FAST
 #define RT_WG_FAST 64                          // workgroup of the default render kernels: 64 (8 x 8) or 128 (16 x 8)
 #endif
+// RT_PIX_RECOMPUTE=1: the store recomputes the pixel position from an opaque copy of the thread index instead of
+// keeping it live through trace(): 2 VGPRs fewer in the culling kernels, but c3 +2.9% (same-box A/B), so off.
+#ifndef RT_PIX_RECOMPUTE
+#define RT_PIX_RECOMPUTE 0
+#endif
 #ifndef RT_MINW_CULL
 #define RT_MINW_CULL 5                         // the culling variant (>= kConeMin spheres): 87 VGPRs, no spills
 #endif
+// Default launch-bound waves per SIMD of the fast kernels by depth: 6 up to depth 2, 5 from depth 3.  The bound
+// is a floor: the depth 0-1 kernels come out at 69-72 VGPRs under it, i.e. 7 waves per SIMD (the c2 kernel
+// accumulates its colour in LDS, shade ACC); a bound of 7 made the compiler trade SGPR spills (v_writelane) for
+// the same 69 VGPRs and ran c2 +2.3% slower (same-box A/B).
+__host__ __device__ constexpr int kDefaultMinWaves(int B) { return B <= 2 ? 6 : 5; }
 // RT_MAX_B < 7 (experiment builds only, tools/variants.sh): deeper kernels are not instantiated.
 #ifndef RT_MAX_B
 #define RT_MAX_B 7
@@ -63,10 +73,11 @@ constexpr int kGridY = 32768;                  // grid.y per grid.z slice
 constexpr int kFmtF_RGBA = 0, kFmtF_GRAY = 1;                // float image
 constexpr int kFmt8_RGBA = 0, kFmt8_RGB = 1, kFmt8_GRAY = 2;  // byte image
 
-// LDS bytes of trace()'s per-level slots for depth B: 3 doubles (+ the material id when TRANSP) per level
-// and work-item of a `wg`-thread workgroup.
+// LDS bytes of trace()'s per-level slots for depth B: 3 doubles per colour slot (colour_slots: one per level,
+// plus one for the parked continuation when the colour accumulates in LDS) and the material id per level when
+// TRANSP, per work-item of a `wg`-thread workgroup.
 __host__ __device__ constexpr int slot_bytes(int B, bool transp, int wg = kSlotStride) {
-    return (B + 1) * (3 * 8 + (transp ? 4 : 0)) * wg;
+    return (colour_slots(B, transp) * 3 * 8 + (transp ? (B + 1) * 4 : 0)) * wg;
 }
 
 struct RenderParams {
@@ -184,7 +195,7 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
         off = P.lds_bytes;
     }
     double* slot = reinterpret_cast<double*>(smem + off) + tid;
-    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * (B + 1) * WG) + tid;
+    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * colour_slots(B, TRANSP) * WG) + tid;
     off += slot_bytes(B, TRANSP, WG);
     float4* st32 = reinterpret_cast<float4*>(smem + off);                              // [8][32] 4 KB
     double* st64 = reinterpret_cast<double*>(smem + off + 4096);                        // [8][32][3] 6 KB
@@ -249,8 +260,14 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
     if (WG != kThreads || !P.wg_staging) {
         // Direct stores: each wave writes its 8 x 8 block as 8 row segments (128 B of RGBA32F each) and
         // retires without waiting at a workgroup barrier for slower waves of the tile.
-        if (valid) {
-            const size_t k = (size_t)lr * P.width + i;
+        int tid_e = tid;
+#if RT_PIX_RECOMPUTE
+        asm volatile("" : "+v"(tid_e));
+#endif
+        const int lane_e = tid_e & 63;
+        const int i_e = tx * TW + (tid_e >> 6) * bw + (lane_e & 7), lr_e = ty * kTileH + (lane_e >> 3);
+        if (i_e < P.width && lr_e < P.local_rows && !pad) {
+            const size_t k = (size_t)lr_e * P.width + i_e;
             store_pixel<PACKED>(P, k, col, out32, out8);
             if (out64) { out64[3 * k] = col.x; out64[3 * k + 1] = col.y; out64[3 * k + 2] = col.z; }
             if (outrc) outrc[k] = seg | (sh << 16);
@@ -308,7 +325,7 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
     const d3 p0 = ld3(starts + 3 * kk);
     V.hits_ok = hits_ok_from(S, p0);
     double* slot = reinterpret_cast<double*>(smem) + threadIdx.x;
-    int* mslot = reinterpret_cast<int*>(smem + 3 * 8 * (B + 1) * kSlotStride) + threadIdx.x;
+    int* mslot = reinterpret_cast<int*>(smem + 3 * 8 * colour_slots(B, TRANSP) * kSlotStride) + threadIdx.x;
     d3 c;
     if constexpr (TREE)
         c = trace_tree<B>(V, p0, ld3(ends + 3 * kk), &seg, &sh);
@@ -391,7 +408,7 @@ hipError_t launch_render_impl(const RenderLaunch& L) {
     if constexpr (B > RT_MAX_B) {
         return hipErrorInvalidValue;
     } else {
-        constexpr int MW = RT_MINW != 0 ? RT_MINW : (B <= 2 ? 6 : 5);     // depth-dependent default
+        constexpr int MW = RT_MINW != 0 ? RT_MINW : kDefaultMinWaves(B);
         switch (L.variant) {
             case kVarFast: return launch_render_one<B, 0, MW, false, false, RT_WG_FAST, false>(L);
             case kVarFastAnyW: return launch_render_one<B, 0, 1, false, false, RT_WG_FAST, false>(L);
@@ -436,7 +453,7 @@ const void* render_kernel_ptr_impl(int variant) {
     if constexpr (B > RT_MAX_B) {
         return nullptr;
     } else {
-        constexpr int kFast = B <= 3 ? (RT_MINW != 0 ? RT_MINW : (B <= 2 ? 6 : 5)) : 1;
+        constexpr int kFast = B <= 3 ? (RT_MINW != 0 ? RT_MINW : kDefaultMinWaves(B)) : 1;
         constexpr int kCull = B <= 3 ? RT_MINW_CULL : 1;
         switch (variant) {
             case 0: return (const void*)rt_render_kernel<B, 0, kFast, false, false, RT_WG_FAST, false>;
