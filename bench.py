@@ -137,7 +137,7 @@ ROCPROF_ONE_STREAM = "profiles/r03/{cfg}_kernel_stats_1stream.csv"
 
 
 def rocprof_reference(cfg_name, full_frame):
-    """The committed one-stream rocprofv3 --kernel-trace --stats summary of this config (tools/gpu_prof_1stream.sh:
+    """The committed one-stream rocprofv3 --kernel-trace --stats summary of this config (PROFILE=1 tools/gpu_r03.sh:
     bench.py --frames-in-flight 1 --profile-kernel-only): AverageNs of rt_render_kernel is the launch duration,
     so bytes / AverageNs / peak reproduces `frac` from profiles/ alone."""
     path = os.path.join(ROOT, ROCPROF_ONE_STREAM.format(cfg=cfg_name))
@@ -568,6 +568,9 @@ def main() -> int:
     prof = rocprof_reference(args.config, nl == H and world == 1)
     if prof:
         roof.update(prof)
+        # the committed profile's frac, and its agreement with the live launch duration
+        roof["frac_rocprof"] = round(roof["achieved"] * launch_ms / (prof["rocprof_avg_us"] / 1e3) / roof["peak"], 5)
+        roof["rocprof_vs_live"] = round(prof["rocprof_avg_us"] / 1e3 / launch_ms, 4)
     if world > 1:
         roof["traffic"] = None                               # the PMC figures are whole-frame, one GPU
 
@@ -683,6 +686,9 @@ def main() -> int:
             prof = rocprof_reference(name, True)
             if prof:
                 confs[name].update(prof)
+                confs[name]["hbm_frac_rocprof"] = round(
+                    r1["algorithmic_bytes_per_launch"] / (prof["rocprof_avg_us"] * 1e-6) / 1e9 / r1["peak"], 5)
+                confs[name]["rocprof_vs_live"] = round(prof["rocprof_avg_us"] / 1e3 / kser, 4)
             t.close()
         res_extra["configs"] = confs
 

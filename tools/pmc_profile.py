@@ -20,7 +20,7 @@ def main():
     cfg, path = sys.argv[1], sys.argv[2]
     note = sys.argv[3] if len(sys.argv) > 3 else ""
     d = json.load(open(path))
-    ks = [k for k in d if k.startswith("rt_render_kernel")]
+    ks = [k for k in d if "rt_render_kernel" in k]
     k = max(ks, key=lambda x: d[x].get("_dispatches", 0))
     c = d[k]
     out = {"config": cfg, "kernel": k,
@@ -39,6 +39,12 @@ def main():
         wi = c[f64[0]] + c[f64[1]] + 2 * c[f64[2]] + c[f64[3]]
         out["fp64_wave_instructions"] = {x.replace("SQ_INSTS_VALU_", ""): c[x] for x in f64}
         out["fp64_flops_issued_per_launch"] = wi * 64
+        if c.get("SQ_INSTS_VALU"):
+            # FP64 share of the issued VALU wave-instructions (each FP64 instruction counted once)
+            n64 = c[f64[0]] + c[f64[1]] + c[f64[2]] + c[f64[3]]
+            out["fp64_share_of_valu"] = round(n64 / c["SQ_INSTS_VALU"], 4)
+            out["valu_per_wave"] = round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1) if c.get("SQ_WAVES") else None
+            out["fp64_per_wave"] = round(n64 / c["SQ_WAVES"], 1) if c.get("SQ_WAVES") else None
     for x in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
               "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "VALUBusy", "VALUUtilization", "GRBM_GUI_ACTIVE"):
         if x in c:
