@@ -35,6 +35,9 @@ int rt_diag_tile_order(rt_ctx* ctx, int mode);
  * lives in scratch by design).  Needs a HIP device.  RT_EINVAL for bad arguments. */
 int rt_diag_kernel_resources(int depth, int variant, int* vgprs, int* scratch_bytes);
 
+/* Workgroups per CU the HIP runtime allows the render kernel (depth, variant) with lds_bytes of dynamic LDS. */
+int rt_diag_kernel_occupancy(int depth, int variant, int lds_bytes, int* blocks_per_cu);
+
 #ifdef __cplusplus
 }
 #endif

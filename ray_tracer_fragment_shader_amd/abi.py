@@ -163,9 +163,10 @@ SIGNATURES = {
     "rt_probe_math_dev": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "rt_diag_tile_order": (c_int, [c_void_p, c_int]),
     "rt_diag_kernel_resources": (c_int, [c_int, c_int, _P(c_int), _P(c_int)]),
+    "rt_diag_kernel_occupancy": (c_int, [c_int, c_int, c_int, _P(c_int)]),
 }
 
-_DIAG = {"rt_diag_tile_order", "rt_diag_kernel_resources"}
+_DIAG = {"rt_diag_tile_order", "rt_diag_kernel_resources", "rt_diag_kernel_occupancy"}
 _lib = None
 
 

@@ -1114,6 +1114,27 @@ extern "C" int rt_diag_kernel_resources(int depth, int variant, int* vgprs, int*
     return RT_OK;
 }
 
+// Workgroups of the render kernel (depth, variant as above) the runtime places per CU with `lds_bytes` of
+// dynamic LDS (hipOccupancyMaxActiveBlocksPerMultiprocessor).
+extern "C" int rt_diag_kernel_occupancy(int depth, int variant, int lds_bytes, int* blocks_per_cu) {
+    if (depth < 0 || depth > RT_MAX_B || variant < 0 || variant > 3 || lds_bytes < 0 || !blocks_per_cu)
+        return rt_fail(RT_EINVAL, "rt_diag_kernel_occupancy: bad arguments");
+    const void* f = nullptr;
+    switch (depth) {
+        case 0: f = render_kernel_ptr<0>(variant); break;
+        case 1: f = render_kernel_ptr<1>(variant); break;
+        case 2: f = render_kernel_ptr<2>(variant); break;
+        case 3: f = render_kernel_ptr<3>(variant); break;
+        case 4: f = render_kernel_ptr<4>(variant); break;
+        case 5: f = render_kernel_ptr<5>(variant); break;
+        case 6: f = render_kernel_ptr<6>(variant); break;
+        default: f = render_kernel_ptr<7>(variant); break;
+    }
+    if (!f) return rt_fail(RT_EINVAL, "rt_diag_kernel_occupancy: kernel not built");
+    RT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, RT_WG_FAST, (size_t)lds_bytes));
+    return RT_OK;
+}
+
 extern "C" int rt_probe_math_dev(int op, const double* in, int n, double* out, void* stream) {
     if (op != 0 && op != 1) return rt_fail(RT_EINVAL, "rt_probe_math_dev: unknown op");
     if (n < 0 || (n > 0 && (!in || !out))) return rt_fail(RT_EINVAL, "rt_probe_math_dev: bad buffers");

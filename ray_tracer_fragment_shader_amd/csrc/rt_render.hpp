@@ -50,9 +50,10 @@
 #define RT_MINW_CULL 5                         // the culling variant (>= kConeMin spheres): 87 VGPRs, no spills
 #endif
 // Default launch-bound waves per SIMD of the fast kernels by depth: 6 up to depth 2, 5 from depth 3.  The bound
-// is a floor: the depth 0-1 kernels come out at 69-72 VGPRs under it, i.e. 7 waves per SIMD (the c2 kernel
-// accumulates its colour in LDS, shade ACC); a bound of 7 made the compiler trade SGPR spills (v_writelane) for
-// the same 69 VGPRs and ran c2 +2.3% slower (same-box A/B).
+// is a floor: the depth 1 kernel comes out at 71 VGPRs under it (7 waves by VGPRs; the c2 kernel accumulates
+// its colour in LDS, shade ACC), but its 106 SGPRs hold it at 6 waves per SIMD on the hardware (see
+// rt_render_kernel_sg); a bound of 7 made the compiler trade SGPR spills (v_writelane) for the same VGPRs and ran
+// c2 +2.3% slower (same-box A/B).
 __host__ __device__ constexpr int kDefaultMinWaves(int B) { return B <= 2 ? 6 : 5; }
 // RT_MAX_B < 7 (experiment builds only, tools/variants.sh): deeper kernels are not instantiated.
 #ifndef RT_MAX_B
@@ -171,12 +172,10 @@ __device__ __forceinline__ void store_pixel(const RenderParams& P, size_t k, d3 
 
 template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false,
           bool PACKED = false>
-__global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
-                                                             RenderParams P, void* __restrict__ out32,
-                                                             void* __restrict__ out8,
-                                                             double* __restrict__ out64,
-                                                             uint32_t* __restrict__ outrc,
-                                                             const int32_t* __restrict__ tile_rows) {
+__device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene, RenderParams P,
+                                            void* __restrict__ out32, void* __restrict__ out8,
+                                            double* __restrict__ out64, uint32_t* __restrict__ outrc,
+                                            const int32_t* __restrict__ tile_rows) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
 #if RT_WAVE_TRACE
@@ -225,6 +224,10 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
     const int i = tx * TW + cx;
     const int lr = ty * kTileH + cy;
     const bool valid = i < P.width && lr < P.local_rows && !pad;
+#if RT_WAVE_TRACE >= 2
+    asm volatile("" ::"s"(ty));
+    const uint64_t t_ty = __builtin_amdgcn_s_memrealtime();   // the tile row has arrived
+#endif
 
     // Per-wave sphere culling (all lanes active here).  The block's rows must be contiguous image rows.
     uint64_t cone = ~0ull;
@@ -240,6 +243,10 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
                                      sqrtf(hx * hx + hy * hy), P.cone_slack, lane);
         RT_COUNT(V.S, kCntConeKept, __popcll(cone & sphere_bits(V.np)));
     }
+#if RT_WAVE_TRACE >= 2
+    asm volatile("" ::"s"(cone));
+    const uint64_t t_cone = __builtin_amdgcn_s_memrealtime();   // the primary cone mask is known
+#endif
 
     // Every lane traces (trace() reduces over the wave): lanes outside the frame trace a clamped pixel
     // and store nothing.
@@ -251,6 +258,9 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
     const d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(ic + P.bottom_x), right)),
                       scl(P.pitch * (double)(j + P.bottom_y), upp));
     const d3 bdP = sub(ld3(V.S->bc), eye);                  // bounding-sphere deltaP for p0 = camera
+#if RT_WAVE_TRACE
+    const uint64_t t_mid = __builtin_amdgcn_s_memrealtime();   // prologue done: the primary ray is formed
+#endif
     d3 col;
     if constexpr (TREE)
         col = trace_tree<B>(V, eye, sp, &seg, &sh);
@@ -277,9 +287,14 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
 #if RT_WAVE_TRACE
         if (P.wtrace && tid == 0) {
             const size_t w = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-            P.wtrace[3 * w] = t_start;
-            P.wtrace[3 * w + 1] = __builtin_amdgcn_s_memrealtime();
-            P.wtrace[3 * w + 2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+            P.wtrace[4 * w] = t_start;
+            P.wtrace[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
+            P.wtrace[4 * w + 3] = t_mid;
+#if RT_WAVE_TRACE >= 2
+            P.wtrace[4 * (size_t)P.tile_rows_n * gridDim.x + 2 * w] = t_ty;
+            P.wtrace[4 * (size_t)P.tile_rows_n * gridDim.x + 2 * w + 1] = t_cone;
+#endif
+            P.wtrace[4 * w + 2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
                                   ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
         }
 #endif
@@ -307,6 +322,34 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
         if (out8) reinterpret_cast<uchar4*>(out8)[k] = st8[tid];
     }
     if (P.row_cost && tid == 0 && !pad) atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
+}
+
+template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false,
+          bool PACKED = false>
+__global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
+                                                             RenderParams P, void* __restrict__ out32,
+                                                             void* __restrict__ out8,
+                                                             double* __restrict__ out64,
+                                                             uint32_t* __restrict__ outrc,
+                                                             const int32_t* __restrict__ tile_rows) {
+    render_body<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED>(gscene, P, out32, out8, out64, outrc, tile_rows);
+}
+
+// The same kernel with its SGPRs capped at RT_FAST_SGPRS (amdgpu_num_sgpr: a constant, hence a kernel of its
+// own).  The hardware keeps a wave's SGPRs in granules of 16 and fits 7 one-wave workgroups per SIMD only up to
+// 96 SGPRs per wave (tools/mb_slots.cpp: 71 VGPRs with 96 SGPRs -> 7 waves, with 98 -> 6) — the compiler's
+// occupancy estimate (7 at 106) assumes a larger SGPR file.  RT_FAST_SGPRS=96 runs the depth <= RT_SG_MAX_B fast
+// kernels with the cap: c2 then holds 7 waves per SIMD (wave trace: 7,168 resident) with 19 SGPRs spilled to
+// VGPR lanes, and measured +1.1% (same-box A/B) — the seventh wave does not pay for the spills, so off.
+#ifndef RT_FAST_SGPRS
+#define RT_FAST_SGPRS 0
+#endif
+template <int B, int MINW, bool CULL, bool PACKED>
+__global__ __launch_bounds__(RT_WG_FAST, MINW) __attribute__((amdgpu_num_sgpr(RT_FAST_SGPRS)))
+void rt_render_kernel_sg(const DevScene* __restrict__ gscene, RenderParams P, void* __restrict__ out32,
+                         void* __restrict__ out8, double* __restrict__ out64, uint32_t* __restrict__ outrc,
+                         const int32_t* __restrict__ tile_rows) {
+    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED>(gscene, P, out32, out8, out64, outrc, tile_rows);
 }
 
 // rayTraceRay on a list of rays Line(starts[k], ends[k]).  Rays from arbitrary starts: whether their hit
@@ -403,6 +446,17 @@ hipError_t launch_render_one(const RenderLaunch& L) {
     return hipGetLastError();
 }
 
+// The SGPR-capped fast kernel (rt_render_kernel_sg) for the depths whose fast kernels fit 7 waves by VGPRs.
+#ifndef RT_SG_MAX_B
+#define RT_SG_MAX_B 1
+#endif
+template <int B, int MINW, bool PACKED>
+hipError_t launch_render_sg(const RenderLaunch& L) {
+    hipLaunchKernelGGL((rt_render_kernel_sg<B, MINW, false, PACKED>), L.grid, dim3(RT_WG_FAST), L.lds, L.stream, L.scene,
+                       L.P, L.o32, L.o8, L.o64, L.orc, L.P.tile_rows);
+    return hipGetLastError();
+}
+
 template <int B>
 hipError_t launch_render_impl(const RenderLaunch& L) {
     if constexpr (B > RT_MAX_B) {
@@ -410,7 +464,9 @@ hipError_t launch_render_impl(const RenderLaunch& L) {
     } else {
         constexpr int MW = RT_MINW != 0 ? RT_MINW : kDefaultMinWaves(B);
         switch (L.variant) {
-            case kVarFast: return launch_render_one<B, 0, MW, false, false, RT_WG_FAST, false>(L);
+            case kVarFast:
+                if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return launch_render_sg<B, MW, false>(L);
+                return launch_render_one<B, 0, MW, false, false, RT_WG_FAST, false>(L);
             case kVarFastAnyW: return launch_render_one<B, 0, 1, false, false, RT_WG_FAST, false>(L);
             case kVarCull: return launch_render_one<B, 0, RT_MINW_CULL, false, true, RT_WG_FAST, false>(L);
             case kVarCullAnyW: return launch_render_one<B, 0, 1, false, true, RT_WG_FAST, false>(L);
@@ -420,6 +476,7 @@ hipError_t launch_render_impl(const RenderLaunch& L) {
             case kVarStaging: return launch_render_one<B, 0, MW, false, false, kThreads, false>(L);
             case kVarStagingAnyW: return launch_render_one<B, 0, 1, false, false, kThreads, false>(L);
             case kVarFastPacked:
+                if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return launch_render_sg<B, MW, true>(L);
                 return launch_render_one<B, 0, (B <= 3 ? MW : 1), false, false, RT_WG_FAST, false, true>(L);
             case kVarCullPacked:
                 return launch_render_one<B, 0, (B <= 3 ? RT_MINW_CULL : 1), false, true, RT_WG_FAST, false, true>(L);
@@ -456,7 +513,9 @@ const void* render_kernel_ptr_impl(int variant) {
         constexpr int kFast = B <= 3 ? (RT_MINW != 0 ? RT_MINW : kDefaultMinWaves(B)) : 1;
         constexpr int kCull = B <= 3 ? RT_MINW_CULL : 1;
         switch (variant) {
-            case 0: return (const void*)rt_render_kernel<B, 0, kFast, false, false, RT_WG_FAST, false>;
+            case 0:
+                if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return (const void*)rt_render_kernel_sg<B, kFast, false, false>;
+                return (const void*)rt_render_kernel<B, 0, kFast, false, false, RT_WG_FAST, false>;
             case 1: return (const void*)rt_render_kernel<B, 0, kCull, false, true, RT_WG_FAST, false>;
             case 2: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, false>;
             case 3: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, true>;

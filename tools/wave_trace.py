@@ -26,7 +26,7 @@ def main():
     t.set_scene(cfg.scene())
     bufs = t.alloc(W, H, rgba32f=True, rgba8=True)
     nwg = ((W + 7) // 8) * ((H + 7) // 8)
-    tr = torch.zeros(nwg * 3, dtype=torch.int64, device="cuda")
+    tr = torch.zeros(nwg * 6, dtype=torch.int64, device="cuda")   # RT_WAVE_TRACE=2: + {tile row, cone} stamps
     lib = abi.lib()
     lib.rt_debug_wave_trace.argtypes = [ctypes.c_void_p]
     for _ in range(3):
@@ -35,10 +35,13 @@ def main():
     assert lib.rt_debug_wave_trace(ctypes.c_void_p(tr.data_ptr())) == 0
     t.render_into(cfg.camera(), W, H, cfg.depth, bufs)
     torch.cuda.synchronize()
-    a = tr.cpu().numpy().reshape(nwg, 3)
-    st, en, hw = a[:, 0], a[:, 1], a[:, 2]
+    ab = tr.cpu().numpy()
+    a = ab[: nwg * 4].reshape(nwg, 4)
+    b = ab[nwg * 4:].reshape(nwg, 2)
+    st, en, hw, md = a[:, 0], a[:, 1], a[:, 2], a[:, 3]
     t0 = st.min()
-    st, en = (st - t0) * 10.0 / 1000.0, (en - t0) * 10.0 / 1000.0       # 100 MHz ticks -> us
+    st, en, md = ((x - t0) * 10.0 / 1000.0 for x in (st, en, md))      # 100 MHz ticks -> us
+    t_ty, t_cone = ((x - t0) * 10.0 / 1000.0 for x in (b[:, 0], b[:, 1]))
     dur = en - st
     hwid = hw & 0xFFFFFFFF
     xcc = (hw >> 32) & 0xF
@@ -51,6 +54,10 @@ def main():
         "config": name, "waves": int(nwg), "span_us": round(float(en.max()), 2),
         "dur_us": {q: round(float(np.percentile(dur, q)), 2) for q in (5, 25, 50, 75, 95, 99, 100)},
         "mean_dur_us": round(float(dur.mean()), 3),
+        "prologue_us": {q: round(float(np.percentile(md - st, q)), 2) for q in (5, 50, 95)},
+        "mean_prologue_us": round(float((md - st).mean()), 3),
+        "mean_to_tile_row_us": round(float((t_ty - st).mean()), 3) if b[:, 0].any() else None,
+        "mean_to_cone_us": round(float((t_cone - st).mean()), 3) if b[:, 0].any() else None,
         "sum_dur_us_per_slot": round(float(dur.sum()) / (256 * 4 * 5), 2),
         "last_start_us": round(float(st.max()), 2),
         "p99_end_us": round(float(np.percentile(en, 99)), 2),
@@ -66,7 +73,7 @@ def main():
     out["dur_by_tile_row_us"] = [round(float(x), 2) for x in d2.mean(axis=1)[:: max(1, rows // 16)]]
     print(json.dumps(out))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    np.savez(os.path.join(ROOT, "gpurun_out", f"wave_trace_{name}.npz"), start_us=st, end_us=en, hw=hw,
+    np.savez(os.path.join(ROOT, "gpurun_out", f"wave_trace_{name}.npz"), start_us=st, end_us=en, hw=hw, mid_us=md,
              tiles_x=(W + 7) // 8, tiles_y=(H + 7) // 8)
 
 
