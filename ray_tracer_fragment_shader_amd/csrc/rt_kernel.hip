@@ -44,6 +44,9 @@ uint64_t* g_wtrace = nullptr;                  // diagnostic build only (tools/w
 // index), so the longest rows are dispatched first and the cheap ones fill the tail (longest-processing-
 // time-first list scheduling).  One workgroup, bitonic sort of (~cost, row) keys in LDS; n <= kOrderMax.
 constexpr int kOrderMax = 8192;
+#ifndef RT_CONE_CACHE_DEFAULT
+#define RT_CONE_CACHE_DEFAULT 1
+#endif
 constexpr int kRecalibrate = 8;                // renders of a moving camera per re-timing of the tile rows
 __global__ __launch_bounds__(1024) void rt_order_kernel(const uint32_t* __restrict__ cost, int n,
                                                         int32_t* __restrict__ order) {
@@ -67,6 +70,17 @@ __global__ __launch_bounds__(1024) void rt_order_kernel(const uint32_t* __restri
         }
     }
     for (int k = threadIdx.x; k < n; k += blockDim.x) order[k] = (int32_t)(key[k] & 0xffffffffu);
+}
+
+// The calibration render's per-tile primary cone masks (by tile: ty * tiles_x + tx) into dispatch order
+// (gy * tiles_x + tx, tile row order[gy]), for the later renders of the same view.
+__global__ __launch_bounds__(256) void rt_cone_permute_kernel(const uint64_t* __restrict__ by_tile,
+                                                              const int32_t* __restrict__ order, int tiles_x,
+                                                              int tiles_y, uint64_t* __restrict__ by_dispatch) {
+    const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= (size_t)tiles_x * tiles_y) return;
+    const int gy = (int)(k / tiles_x), tx = (int)(k - (size_t)gy * tiles_x);
+    by_dispatch[k] = by_tile[(size_t)order[gy] * tiles_x + tx];
 }
 
 // Per-eye primary-ray sphere data (run by rt_render_dev when the camera eye changes): deltaP = C - eye
@@ -377,6 +391,17 @@ struct rt_ctx {
     ViewKey seen_key{};
     int stale = 0;                             // renders of other cameras since the order was calibrated
     int order_mode = 0;
+    // Primary cone masks of the calibrated view (scenes with >= kPrimaryConeMin spheres): the calibration render
+    // writes each tile's mask (d_cone_tile), rt_cone_permute_kernel puts them in dispatch order (d_cone_disp),
+    // and later renders of exactly that view (order_key) read them instead of recomputing them.  Renders of
+    // another camera compute their own.  d_cone_disp is rewritten only after the device has drained every
+    // render queued with it (cone_readers), whatever stream it went to.
+    uint64_t* d_cone_tile = nullptr;
+    uint64_t* d_cone_disp = nullptr;
+    size_t cone_cap = 0;                       // tiles each holds
+    bool cone_valid = false;                   // d_cone_disp holds the masks of view order_key
+    bool cone_readers = false;                 // a render reading d_cone_disp was queued since the last drain
+    int cone_cache = RT_CONE_CACHE_DEFAULT;    // RT_CONE_CACHE=0: always compute the masks in the kernel (A/B)
     uint64_t scene_gen = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // The host-buffer calls (rt_render, rt_render_packed, rt_render_packed_async) run on the context's own
@@ -438,6 +463,8 @@ extern "C" int rt_ctx_destroy(rt_ctx* c) {
     if (c->d_scene) (void)hipFree(c->d_scene);
     if (c->d_tile_rows) (void)hipFree(c->d_tile_rows);
     if (c->d_row_cost) (void)hipFree(c->d_row_cost);
+    if (c->d_cone_tile) (void)hipFree(c->d_cone_tile);
+    if (c->d_cone_disp) (void)hipFree(c->d_cone_disp);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (int b = 0; b < 2; ++b) {
@@ -468,6 +495,7 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_TILE_ORDER")) c->order_mode = atoi(e) == 1 ? 1 : 0;   // 1: bottom-to-top (A/B)
     if (const char* e = getenv("RT_COPY_MODE")) c->copy_mode = atoi(e) == 0 ? 0 : 1;
     if (const char* e = getenv("RT_COPY_KERNEL")) c->copy_kernel = atoi(e) != 0;
+    if (const char* e = getenv("RT_CONE_CACHE")) c->cone_cache = atoi(e) != 0;
     if (hipMalloc(&c->d_tile_rows, sizeof(int32_t) * kOrderMax) != hipSuccess ||
         hipMalloc(&c->d_row_cost, sizeof(uint32_t) * kOrderMax) != hipSuccess) {
         rt_ctx_destroy(c);
@@ -635,6 +663,7 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
     const int tiles_x = (W + tw - 1) / tw;
     const int tiles_y = (P.local_rows + kTileH - 1) / kTileH;
     P.tile_rows_n = tiles_y;
+    P.tiles_x = tiles_x;
     hipStream_t st = (hipStream_t)stream;
     // A render captured into a hipGraph must be self-contained: it always prepares its eye's data and uses
     // the identity tile-row order (the context's order buffer belongs to whatever view it last calibrated).
@@ -642,7 +671,7 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
     RT_HIP(hipStreamIsCapturing(st, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
     if (capturing) c->ever_captured = true;
-    bool calibrate = false;
+    bool calibrate = false, cone_calib = false;
     rt_ctx::ViewKey key{};
     if (!capturing && c->order_mode == 0 && tiles_y <= c->n_tile_rows) {
         // Key of the frame's work: camera, size, outputs, row plan, depth and scene generation.
@@ -662,6 +691,10 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
                                 memcmp(key.data() + kCam, c->order_key.data() + kCam, key.size() - kCam) == 0;
         if (c->order_valid && key == c->order_key) {
             P.tile_rows = c->d_tile_rows;
+            if (c->cone_valid) {
+                P.cone_in = c->d_cone_disp;
+                c->cone_readers = true;
+            }
         } else if (same_shape) {
             P.tile_rows = c->d_tile_rows;               // another camera: the last calibrated order
             if (++c->stale >= kRecalibrate) {           // ... re-timed every kRecalibrate-th render
@@ -675,10 +708,37 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
             P.row_cost = c->d_row_cost;                 // calibration render (identity order)
             calibrate = true;
             c->order_valid = false;                     // rt_order_kernel rewrites d_tile_rows below
+            cone_calib = c->cone_cache && c->n_padded >= kPrimaryConeMin && !c->tree && !c->transparent;
         } else {
             c->seen_key = key;                          // first render of this view: identity order
             c->seen_valid = true;
         }
+    }
+    if (calibrate) c->cone_valid = false;
+    if (cone_calib) {
+        // this (static) view's calibration also records its cone masks; the buffers may still be read by
+        // renders queued earlier on any stream: drain the device first when one was
+        const size_t need = (size_t)tiles_x * tiles_y;
+        if (c->cone_readers || need > c->cone_cap) {
+            RT_HIP(hipDeviceSynchronize());
+            c->cone_readers = false;
+        }
+        if (need > c->cone_cap) {
+            if (c->d_cone_tile) (void)hipFree(c->d_cone_tile);
+            if (c->d_cone_disp) (void)hipFree(c->d_cone_disp);
+            c->d_cone_tile = c->d_cone_disp = nullptr;
+            c->cone_cap = 0;
+            if (hipMalloc(&c->d_cone_tile, need * sizeof(uint64_t)) != hipSuccess ||
+                hipMalloc(&c->d_cone_disp, need * sizeof(uint64_t)) != hipSuccess) {
+                if (c->d_cone_tile) (void)hipFree(c->d_cone_tile);
+                c->d_cone_tile = nullptr;
+                cone_calib = false;                     // no cache: later renders compute their masks
+                (void)hipGetLastError();
+            } else {
+                c->cone_cap = need;
+            }
+        }
+        if (cone_calib) P.cone_out = c->d_cone_tile;
     }
     const dim3 grid((unsigned)tiles_x, (unsigned)std::min(tiles_y, kGridY), (unsigned)((tiles_y + kGridY - 1) / kGridY));
     hipError_t e;
@@ -742,8 +802,16 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
         hipLaunchKernelGGL(rt_order_kernel, dim3(1), dim3(1024), 0, st, c->d_row_cost, tiles_y, c->d_tile_rows);
         e = hipGetLastError();
         if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_order_kernel: ") + hipGetErrorString(e));
+        if (cone_calib) {
+            const size_t n = (size_t)tiles_x * tiles_y;
+            hipLaunchKernelGGL(rt_cone_permute_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                               c->d_cone_tile, c->d_tile_rows, tiles_x, tiles_y, c->d_cone_disp);
+            e = hipGetLastError();
+            if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_cone_permute_kernel: ") + hipGetErrorString(e));
+        }
         c->order_key = key;                             // only once the order kernel is queued
         c->order_valid = true;
+        c->cone_valid = cone_calib;
         c->stale = 0;
     }
     return RT_OK;

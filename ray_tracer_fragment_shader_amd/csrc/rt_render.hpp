@@ -104,7 +104,10 @@ struct RenderParams {
     const int32_t* tile_rows;                  // dispatch order of tile rows (nullptr: bottom to top)
     uint32_t* row_cost;                        // calibration render: per tile row, sum of wave times (100 MHz)
     int32_t tile_rows_n;                       // tile rows of this launch
+    int32_t tiles_x;                           // tiles per tile row (= grid.x)
     uint64_t* wtrace;                          // RT_WAVE_TRACE builds: per-wave {start, end, HW_ID}
+    const uint64_t* cone_in;                   // this view's primary cone masks in dispatch order (or nullptr)
+    uint64_t* cone_out;                        // calibration render: each tile's mask, by tile (or nullptr)
 };
 
 // Image row (within its frame) of local row lr; local rows are frame-major (rt_rows.frames).
@@ -175,7 +178,8 @@ template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, b
 __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene, RenderParams P,
                                             void* __restrict__ out32, void* __restrict__ out8,
                                             double* __restrict__ out64, uint32_t* __restrict__ outrc,
-                                            const int32_t* __restrict__ tile_rows) {
+                                            const int32_t* __restrict__ tile_rows,
+                                            const uint64_t* __restrict__ cone_in) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
 #if RT_WAVE_TRACE
@@ -219,11 +223,20 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     // Padding tiles of the last grid.z slice trace a clamped tile and store nothing (no early return: a branch
     // here kept the compiler from issuing the scene loads until the tile row had arrived).
     const int ty_raw = tile_rows ? tile_rows[gy] : gy;
+    // The cached primary cone mask of this dispatch position (cone_in: see below), requested together with the
+    // tile row and waited for with it (the empty asm needs both), so the cache costs no round trip of its own;
+    // without a cache the load reads the scene header instead (a valid address) and the value is unused.
+    // (positions past the last tile row — grid.z padding — read the last row's entry: in bounds, unused)
+    const int gyc = gy < P.tile_rows_n ? gy : P.tile_rows_n - 1;
+    const uint64_t* cone_p = cone_in ? cone_in + ((size_t)gyc * P.tiles_x + tx) : reinterpret_cast<const uint64_t*>(gscene);
+    const uint64_t cone_cached = *cone_p;
+    asm volatile("" ::"s"(cone_cached), "s"(ty_raw));
     const bool pad = (unsigned)ty_raw >= (unsigned)P.tile_rows_n;
     const int ty = pad ? P.tile_rows_n - 1 : ty_raw;
     const int i = tx * TW + cx;
     const int lr = ty * kTileH + cy;
     const bool valid = i < P.width && lr < P.local_rows && !pad;
+    (void)valid;                                   // (the direct stores recompute it from i_e, lr_e)
 #if RT_WAVE_TRACE >= 2
     asm volatile("" ::"s"(ty));
     const uint64_t t_ty = __builtin_amdgcn_s_memrealtime();   // the tile row has arrived
@@ -232,7 +245,12 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     // Per-wave sphere culling (all lanes active here).  The block's rows must be contiguous image rows.
     uint64_t cone = ~0ull;
     RT_COUNT(V.S, kCntWaves, 1);
-    if (P.np >= kPrimaryConeMin) {
+    if (P.np >= kPrimaryConeMin && cone_in) {
+        // the mask this view's calibration render computed for this tile, permuted into dispatch order
+        // (rt_cone_permute_kernel): one 8-byte scalar load (a const __restrict__ kernel argument, like
+        // tile_rows) instead of the cone phase
+        cone = cone_cached;
+    } else if (P.np >= kPrimaryConeMin) {
         // Within one frame global_row_of is increasing, so jb - ja == 7 means 8 consecutive rows.
         const int lr0 = ty * kTileH + by0, ja = global_row_of(P, lr0), jb = global_row_of(P, lr0 + bh - 1);
         const bool one_frame = P.frames <= 1 || lr0 / P.frame_rows == (lr0 + bh - 1) / P.frame_rows;
@@ -242,6 +260,7 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
                                      (float)(tx * TW + bx0 + P.bottom_x) + hx, (float)(ja + P.bottom_y) + hy,
                                      sqrtf(hx * hx + hy * hy), P.cone_slack, lane);
         RT_COUNT(V.S, kCntConeKept, __popcll(cone & sphere_bits(V.np)));
+        if (P.cone_out && tid == 0 && !pad) P.cone_out[(size_t)ty * P.tiles_x + tx] = cone;   // lane 0, vector store
     }
 #if RT_WAVE_TRACE >= 2
     asm volatile("" ::"s"(cone));
@@ -331,8 +350,10 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
                                                              void* __restrict__ out8,
                                                              double* __restrict__ out64,
                                                              uint32_t* __restrict__ outrc,
-                                                             const int32_t* __restrict__ tile_rows) {
-    render_body<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED>(gscene, P, out32, out8, out64, outrc, tile_rows);
+                                                             const int32_t* __restrict__ tile_rows,
+                                                             const uint64_t* __restrict__ cone_in) {
+    render_body<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED>(gscene, P, out32, out8, out64, outrc, tile_rows,
+                                                              cone_in);
 }
 
 // The same kernel with its SGPRs capped at RT_FAST_SGPRS (amdgpu_num_sgpr: a constant, hence a kernel of its
@@ -348,8 +369,9 @@ template <int B, int MINW, bool CULL, bool PACKED>
 __global__ __launch_bounds__(RT_WG_FAST, MINW) __attribute__((amdgpu_num_sgpr(RT_FAST_SGPRS)))
 void rt_render_kernel_sg(const DevScene* __restrict__ gscene, RenderParams P, void* __restrict__ out32,
                          void* __restrict__ out8, double* __restrict__ out64, uint32_t* __restrict__ outrc,
-                         const int32_t* __restrict__ tile_rows) {
-    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED>(gscene, P, out32, out8, out64, outrc, tile_rows);
+                         const int32_t* __restrict__ tile_rows, const uint64_t* __restrict__ cone_in) {
+    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED>(gscene, P, out32, out8, out64, outrc, tile_rows,
+                                                                    cone_in);
 }
 
 // rayTraceRay on a list of rays Line(starts[k], ends[k]).  Rays from arbitrary starts: whether their hit
@@ -442,7 +464,7 @@ hipError_t launch_render_one(const RenderLaunch& L) {
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(kern, L.grid, dim3(WG), L.lds, L.stream, L.scene, L.P, L.o32, L.o8, L.o64, L.orc,
-                       L.P.tile_rows);
+                       L.P.tile_rows, L.P.cone_in);
     return hipGetLastError();
 }
 
@@ -453,7 +475,7 @@ hipError_t launch_render_one(const RenderLaunch& L) {
 template <int B, int MINW, bool PACKED>
 hipError_t launch_render_sg(const RenderLaunch& L) {
     hipLaunchKernelGGL((rt_render_kernel_sg<B, MINW, false, PACKED>), L.grid, dim3(RT_WG_FAST), L.lds, L.stream, L.scene,
-                       L.P, L.o32, L.o8, L.o64, L.orc, L.P.tile_rows);
+                       L.P, L.o32, L.o8, L.o64, L.orc, L.P.tile_rows, L.P.cone_in);
     return hipGetLastError();
 }
 

@@ -1,0 +1,113 @@
+"""GPU tests of the per-view primary cone-mask cache (rt_kernel.hip render_dev_impl, rt_cone_permute_kernel):
+the calibration render of a static view records each 8x8 tile's primary-ray sphere mask, later renders of
+exactly that view read it (one scalar load) instead of recomputing it, and renders of any other camera
+compute their own.  The masks only skip spheres a tile's rays provably miss, so every frame must stay
+bit-exact with the reference (MySdlApplication.cpp:1184-1249 via the golden manifest) whichever path made
+its mask — first render, calibration, cached, other camera, back to the cached view, across streams."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import pyoracle as po  # noqa: E402
+from ray_tracer_fragment_shader_amd import abi, scenes  # noqa: E402
+from ray_tracer_fragment_shader_amd.tracer import Tracer  # noqa: E402
+
+from . import golden  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def tr():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a HIP device")
+    t = Tracer(0)
+    yield t
+    t.close()
+
+
+def _hash(b):
+    return f"{po.fnv1a64(b['rgb64f'].cpu().numpy()):016x}"
+
+
+def _moved(cfg, ang):
+    cam = cfg.camera()
+    cam.eye = abi.vec3((60.0 * np.sin(ang), 100.0 + 10.0 * np.cos(ang), 200.0))
+    return cam
+
+
+@pytest.mark.parametrize("name", ["c2", "c3", "c5"])
+def test_static_view_frames_hash_to_the_reference(tr, name):
+    """Renders 1 (identity order, masks computed), 2 (calibration: masks recorded) and 3-5 (masks read from the
+    cache, longest-first order) of one view: every frame is the reference's (manifest hash)."""
+    cfg = scenes.CONFIGS[name]
+    tr.set_scene(cfg.scene())
+    want = golden.manifest()["frames"][name]["fnv1a64"]
+    for k in range(5):
+        b = tr.render(cfg.camera(), cfg.width, cfg.height, cfg.depth, rgba32f=False, rgb64f=True)
+        torch.cuda.synchronize()
+        assert _hash(b) == want, f"render {k}"
+
+
+def test_other_cameras_and_back(tr):
+    """A cached view, then cameras of the same frame shape (their own masks, the calibrated order reused and
+    re-timed every 8th render), then the cached view again: each frame equals a fresh context's first render
+    of that camera, and the cached view still hashes to the reference."""
+    cfg = scenes.CONFIGS["c2"]
+    W, H = cfg.width, cfg.height
+    sc = cfg.scene()
+    tr.set_scene(sc)
+    want = golden.manifest()["frames"]["c2"]["fnv1a64"]
+    for _ in range(3):
+        b = tr.render(cfg.camera(), W, H, cfg.depth, rgba32f=False, rgb64f=True)
+    views = [_moved(cfg, 2.0 * np.pi * v / 12) for v in range(12)]
+    got = []
+    for v in views:
+        b = tr.render(v, W, H, cfg.depth, rgba32f=False, rgb64f=True)
+        got.append(b["rgb64f"].clone())
+    b = tr.render(cfg.camera(), W, H, cfg.depth, rgba32f=False, rgb64f=True)
+    torch.cuda.synchronize()
+    assert _hash(b) == want
+    fresh = Tracer(0)
+    try:
+        fresh.set_scene(sc)
+        for v, g in zip(views, got):
+            ref = fresh.render(v, W, H, cfg.depth, rgba32f=False, rgb64f=True)["rgb64f"]
+            torch.cuda.synchronize()
+            assert torch.equal(g, ref)
+    finally:
+        fresh.close()
+
+
+def test_view_change_with_renders_in_flight_on_other_streams(tr):
+    """Cached renders of view A queued on one stream, then view B rendered twice on another stream (its
+    calibration rewrites the cache while A's renders may still be running: the context drains the device
+    first), then A again: every A frame hashes to the reference, B equals a fresh context's render."""
+    cfg = scenes.CONFIGS["c3"]
+    W, H = cfg.width, cfg.height
+    sc = cfg.scene()
+    tr.set_scene(sc)
+    want = golden.manifest()["frames"]["c3"]["fnv1a64"]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(3):
+        tr.render(cfg.camera(), W, H, cfg.depth, rgba32f=False, rgb64f=True, stream=s1)
+    torch.cuda.synchronize()
+    bufs = [tr.alloc(W, H, rgba32f=False, rgb64f=True) for _ in range(4)]
+    for b in bufs[:3]:
+        tr.render_into(cfg.camera(), W, H, cfg.depth, b, stream=s1)
+    vb = _moved(cfg, 1.0)
+    tr.render(vb, W, H, cfg.depth, rgba32f=False, rgb64f=True, stream=s2)
+    b_frame = tr.render(vb, W, H, cfg.depth, rgba32f=False, rgb64f=True, stream=s2)
+    tr.render_into(cfg.camera(), W, H, cfg.depth, bufs[3], stream=s1)
+    torch.cuda.synchronize()
+    for k, b in enumerate(bufs):
+        assert _hash(b) == want, f"A frame {k}"
+    fresh = Tracer(0)
+    try:
+        fresh.set_scene(sc)
+        ref = fresh.render(vb, W, H, cfg.depth, rgba32f=False, rgb64f=True)["rgb64f"]
+        torch.cuda.synchronize()
+        assert torch.equal(b_frame["rgb64f"], ref)
+    finally:
+        fresh.close()
