@@ -588,9 +588,19 @@ __device__ __forceinline__ uint64_t sphere_bits(int np) { return np >= 64 ? ~0ul
 // Spheres go in batches of kChunk: the FP32 filter of the whole batch is evaluated branch-free (records
 // in SGPRs), then each lane runs the exact FP64 test only on its own surviving spheres, in increasing k,
 // so the strict-< closest-hit order of the reference is unchanged.  Padding spheres never survive.
+#ifndef RT_SEC_PREFETCH
+#define RT_SEC_PREFETCH 0
+#endif
 __device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const Ray& r, int k0, double eps,
                                                      int* kind, double* best, d3* hp, int self = -1) {
     uint32_t pass = 0;
+#if RT_SEC_PREFETCH
+    // the batch's exact-test records requested with its filter records (one wait for all)
+    DevSphere sp4[kChunk];
+#pragma unroll
+    for (int j = 0; j < kChunk; ++j) sp4[j] = V.sph[k0 + j];
+    asm volatile("" ::"s"(sp4[0].r2), "s"(sp4[1].r2), "s"(sp4[2].r2), "s"(sp4[3].r2));
+#endif
 #pragma unroll
     for (int j = 0; j < kChunk; ++j) pass |= (sphere_reject32(V.sphf[k0 + j], r) ? 0u : 1u) << j;
     pass = drop_self(pass, self, k0);                       // r starts on sphere `self`: a certain miss
@@ -599,6 +609,20 @@ __device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const R
     for (int j = 0; j < kChunk; ++j) {
         if (!(pass & (1u << j))) continue;                  // skipped by the wave when no lane needs it
         const int k = k0 + j;
+#if RT_SEC_PREFETCH
+        {
+            d3 q;
+            if (sphere_hit(sp4[j], r.p0, r.u, eps, &q)) {
+                double dist = len_fast(sub(q, r.p0));            // :811-812
+                if (dist < *best || *best < 0.0) {          // :813
+                    *best = dist;
+                    *kind = 1 + k;
+                    *hp = q;
+                }
+            }
+            continue;
+        }
+#endif
 #else
     while (pass) {
         const int k = k0 + __builtin_ctz(pass);
@@ -641,10 +665,19 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
         for (uint64_t m = mask & sphere_bits(V.np); m; m &= m - 1) {
             const int k = __builtin_ctzll(m);
             RT_COUNT(S, kCntFilterRay, 1);
+#if RT_PRIM_PREFETCH
+            // the exact test's record with the filter's (one wait for both, as in primary_sphere)
+            const DevSphereF sf = V.sphf[k];
+            const DevSphere sp = V.sph[k];
+            asm volatile("" ::"s"(sf.rm), "s"(sp.r2));
+            if (k == skip - 1 || sphere_reject32(sf, r)) continue;
+#else
             if (k == skip - 1 || sphere_reject32(V.sphf[k], r)) continue;
+            const DevSphere& sp = V.sph[k];
+#endif
             RT_COUNT(S, kCntExactRay, 1);
             d3 q;
-            if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) {
+            if (sphere_hit(sp, r.p0, r.u, eps, &q)) {
                 double dist = len_fast(sub(q, r.p0));       // :811-812
                 if (dist < best || best < 0.0) {            // :813
                     best = dist;
@@ -665,17 +698,30 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
 // cull makes the whole g_scene a miss, whatever the children say, so it can be tested after them.
 // One sphere of a primary ray: FP32 filter on the per-eye image, then the exact test (:747-772) and the
 // strict-< closest-hit update (:811-813).
+#ifndef RT_PRIM_PREFETCH
+#define RT_PRIM_PREFETCH 0
+#endif
 __device__ __forceinline__ void primary_sphere(const SceneView& V, const Ray& r, int k, double eps, int* kind,
                                                double* best, d3* hp) {
-    const DevSpherePrimF& f = V.primf[k];
+    const DevSpherePrimF f = V.primf[k];
+#if RT_PRIM_PREFETCH
+    // The exact test's records are requested with the filter's (scalar loads, one wait for all): a sphere that
+    // passes the filter then costs no second round trip to memory.
+    const DevSpherePrim pp = V.prim[k];
+    const double r2 = V.sph[k].r2;
+    asm volatile("" ::"s"(f.c0), "s"(pp.dd), "s"(r2));
+#endif
     float uD = r.ux * f.dx;
     uD = fmaf(r.uy, f.dy, uD);
     uD = fmaf(r.uz, f.dz, uD);
     if (fmaf(uD, uD, f.c0) < 0.0f) return;                  // certain disc < 0
+#if !RT_PRIM_PREFETCH
     const DevSpherePrim& pp = V.prim[k];
+    const double r2 = V.sph[k].r2;
+#endif
     d3 q;
     RT_COUNT(V.S, kCntExactPrimary, 1);
-    if (sphere_hit_dp(ld3(pp.dP), pp.dd, V.sph[k].r2, r.p0, r.u, eps, &q)) {
+    if (sphere_hit_dp(ld3(pp.dP), pp.dd, r2, r.p0, r.u, eps, &q)) {
         double dist = len_fast(sub(q, r.p0));
         if (dist < *best || *best < 0.0) {
             *best = dist;
