@@ -73,14 +73,15 @@ __global__ __launch_bounds__(1024) void rt_order_kernel(const uint32_t* __restri
 }
 
 // The calibration render's per-tile primary cone masks (by tile: ty * tiles_x + tx) into dispatch order
-// (gy * tiles_x + tx, tile row order[gy]), for the later renders of the same view.
+// (position gy * tiles_x + tx, tile row order[gy], stored at cone_slot: grouped by XCD), for the later renders
+// of the same view.
 __global__ __launch_bounds__(256) void rt_cone_permute_kernel(const uint64_t* __restrict__ by_tile,
                                                               const int32_t* __restrict__ order, int tiles_x,
                                                               int tiles_y, uint64_t* __restrict__ by_dispatch) {
-    const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (k >= (size_t)tiles_x * tiles_y) return;
+    const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x, n = (size_t)tiles_x * tiles_y;
+    if (k >= n) return;
     const int gy = (int)(k / tiles_x), tx = (int)(k - (size_t)gy * tiles_x);
-    by_dispatch[k] = by_tile[(size_t)order[gy] * tiles_x + tx];
+    by_dispatch[cone_slot(k, n)] = by_tile[(size_t)order[gy] * tiles_x + tx];
 }
 
 // Per-eye primary-ray sphere data (run by rt_render_dev when the camera eye changes): deltaP = C - eye
@@ -718,7 +719,7 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
     if (cone_calib) {
         // this (static) view's calibration also records its cone masks; the buffers may still be read by
         // renders queued earlier on any stream: drain the device first when one was
-        const size_t need = (size_t)tiles_x * tiles_y;
+        const size_t need = cone_slots((size_t)tiles_x * tiles_y);
         if (c->cone_readers || need > c->cone_cap) {
             RT_HIP(hipDeviceSynchronize());
             c->cone_readers = false;

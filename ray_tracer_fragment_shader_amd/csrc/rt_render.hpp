@@ -81,6 +81,12 @@ __host__ __device__ constexpr int slot_bytes(int B, bool transp, int wg = kSlotS
     return (colour_slots(B, transp) * 3 * 8 + (transp ? (B + 1) * 4 : 0)) * wg;
 }
 
+// Slot of dispatch position L (linear workgroup id) in the cached cone-mask buffer of n positions: grouped by
+// L mod 8, the XCD the round-robin dispatcher sends workgroup L to (up to a per-launch rotation), so each XCD
+// reads a contiguous run of the buffer and no L2 line is fetched by more than one XCD.
+__host__ __device__ __forceinline__ size_t cone_slot(size_t L, size_t n) { return (L & 7) * ((n + 7) >> 3) + (L >> 3); }
+__host__ __device__ __forceinline__ size_t cone_slots(size_t n) { return ((n + 7) >> 3) << 3; }
+
 struct RenderParams {
     double eye[3];
     double look[3];
@@ -228,7 +234,8 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     // without a cache the load reads the scene header instead (a valid address) and the value is unused.
     // (positions past the last tile row — grid.z padding — read the last row's entry: in bounds, unused)
     const int gyc = gy < P.tile_rows_n ? gy : P.tile_rows_n - 1;
-    const uint64_t* cone_p = cone_in ? cone_in + ((size_t)gyc * P.tiles_x + tx) : reinterpret_cast<const uint64_t*>(gscene);
+    const uint64_t* cone_p = cone_in ? cone_in + cone_slot((size_t)gyc * P.tiles_x + tx, (size_t)P.tile_rows_n * P.tiles_x)
+                                     : reinterpret_cast<const uint64_t*>(gscene);
     const uint64_t cone_cached = *cone_p;
     asm volatile("" ::"s"(cone_cached), "s"(ty_raw));
     const bool pad = (unsigned)ty_raw >= (unsigned)P.tile_rows_n;
