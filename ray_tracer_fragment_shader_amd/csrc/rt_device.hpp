@@ -1113,6 +1113,9 @@ __device__ __forceinline__ d3 transmitted_end(const SceneView& V, int kind, int 
 }
 
 // Surface data of a hit: normal, material id, reflected end point p + r (:679-683, :774-778, :1101-1111).
+#ifndef RT_CENTER_UNIFORM
+#define RT_CENTER_UNIFORM 0
+#endif
 __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u, d3* n, int* mat, d3* pe) {
     const DevScene* S = V.S;
     if (kind == 0) {
@@ -1121,7 +1124,23 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
         const DevMesh& M = V.mesh[(kind - kMeshKind) >> 4];
         *n = ld3(V.tri[M.tri0 + ((kind - kMeshKind) & 15)].n);
     } else {
+#if RT_CENTER_UNIFORM
+        // the centres of the spheres this wave hit, one scalar load per distinct sphere (the first remaining
+        // lane's), instead of a per-lane vector load
+        d3 c = mk(0.0, 0.0, 0.0);
+        bool todo = true;
+        for (;;) {
+            const uint64_t m = __ballot(todo);
+            if (m == 0) break;
+            const int k = __builtin_amdgcn_readlane(kind, (int)__builtin_ctzll(m));
+            if (todo && kind == k) {
+                c = ld3(V.sph[k - 1].c);
+                todo = false;
+            }
+        }
+#else
         d3 c = ld3(V.sph[kind - 1].c);
+#endif
         d3 dp = sub(p, c);                                  // directionP0 (:763)
         *n = unit(dp);                                      // :774-775
     }
@@ -1136,6 +1155,9 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
 // FULL: meshes may be present and materials may be transparent (closest-hit shadows, :1219-1221).
 // ACC: the colour is accumulated in LDS at acc[0], acc[SS], acc[2 SS] (starting at 0, the same additions in the
 // same order) instead of in registers live across every light's shadow test; the return value is then unused.
+#ifndef RT_MAT_UNIFORM
+#define RT_MAT_UNIFORM 0
+#endif
 template <bool FULL, bool CULL, bool ACC = false, int SS = 256>
 __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, int mat, double ks,
                                     int skip = -1, double* acc = nullptr) {
@@ -1161,10 +1183,34 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
         bool lit = false;
         if (hit) lit = !(FULL ? occluded_transparent(V, sr) : occluded<false, CULL>(V, sr, i, m, skip));
         if (lit) {
-            const DevMat& M = S->mat[mat];                  // material terms loaded only when lit
             double a = S->att / (S->att + dl * dl);         // attenuation (:1181)
             d3 lC = scl(a, ld3(S->light[i].col));           // :1223
+#if RT_MAT_UNIFORM
+            // Opaque scenes use materials 0-2 (board squares, spheres): each one some lit lane needs is read with
+            // scalar loads (wave-uniform address) and selected per lane, instead of a per-lane vector load.
+            d3 amb = mk(0.0, 0.0, 0.0), dif = amb, spc = amb;
+            if (!FULL) {
+#pragma unroll
+                for (int m = 0; m < 3; ++m) {
+                    if (__ballot(mat == m) == 0) continue;
+                    const DevMat& M = S->mat[m];
+                    if (mat == m) {
+                        amb = ld3(M.amb);
+                        dif = ld3(M.diff);
+                        spc = ld3(M.spec);
+                    }
+                }
+            } else {
+                const DevMat& M = S->mat[mat];
+                amb = ld3(M.amb);
+                dif = ld3(M.diff);
+                spc = ld3(M.spec);
+            }
+            d3 term = add(add(had(amb, lC), scl(kd, had(dif, lC))), scl(ks, had(spc, lC)));
+#else
+            const DevMat& M = S->mat[mat];                  // material terms loaded only when lit
             d3 term = add(add(had(ld3(M.amb), lC), scl(kd, had(ld3(M.diff), lC))), scl(ks, had(ld3(M.spec), lC)));
+#endif
             if (ACC) {                                      // :1224-1226, in LDS
                 acc[0] = acc[0] + term.x;
                 acc[SS] = acc[SS] + term.y;
