@@ -31,3 +31,16 @@ int rt_unshuffle_dev_ex(const void* gathered, const void* rank0_slab, void* imag
 // rt_unpack_dev with rank 0's rows read from `rank0_slab` (as rt_unshuffle_dev_ex).
 int rt_unpack_dev_ex(const void* gathered, const void* rank0_slab, void* image, int W, int H, int src_format,
                      int dst_format, int band_height, int n_ranks, int slab_rows, void* stream);
+
+// rt_render_screen's device-side ray formation (rt_kernel.hip).  One pixel of a chunk: its screen point and
+// the window of jitter-stream samples traced for it (stream indices base .. base + len - 1, relative to the
+// chunk's first stream index), whose rays occupy ends[off .. off + len - 1].
+struct ScreenPix {
+    double sp[3];
+    int32_t base, len, off, pad;
+};
+constexpr int kScreenMaxWindow = 128;          // len <= this (one workgroup per pixel)
+// ends[off + j] = sp + 0.5 * jit[base + j] for every pixel of `pix` (device-visible), j < len (MSA:1296).
+int rt_screen_form_ends(const ScreenPix* pix, int m, const double* jit, double* ends, void* stream);
+// out[k] = p for k < n (the rays' common start, the camera).
+int rt_fill_points(double* out, int n, const double p[3], void* stream);

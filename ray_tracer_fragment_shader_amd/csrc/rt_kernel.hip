@@ -1204,6 +1204,46 @@ extern "C" int rt_diag_kernel_occupancy(int depth, int variant, int lds_bytes, i
     return RT_OK;
 }
 
+// rt_render_screen's jittered rays, formed on the device: ray j of pixel q ends at sp_q + 0.5 * jitter[base_q + j]
+// (ray.set(camera, screenPt + .5 * randomUnit()), MSA:1296; 0.5 * x is exact and the sum rounds as the host's).
+__global__ __launch_bounds__(kScreenMaxWindow) void rt_screen_ends_kernel(const ScreenPix* __restrict__ pix,
+                                                                         const double* __restrict__ jit,
+                                                                         double* __restrict__ ends) {
+    const ScreenPix& P = pix[blockIdx.x];
+    const int j = threadIdx.x;
+    if (j >= P.len) return;
+    const double* J = jit + 3 * (size_t)(P.base + j);
+    double* e = ends + 3 * (size_t)(P.off + j);
+    e[0] = P.sp[0] + 0.5 * J[0];
+    e[1] = P.sp[1] + 0.5 * J[1];
+    e[2] = P.sp[2] + 0.5 * J[2];
+}
+
+__global__ __launch_bounds__(256) void rt_fill_points_kernel(double* __restrict__ out, int n, double x, double y,
+                                                             double z) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    out[3 * k] = x;
+    out[3 * k + 1] = y;
+    out[3 * k + 2] = z;
+}
+
+int rt_screen_form_ends(const ScreenPix* pix, int m, const double* jit, double* ends, void* stream) {
+    if (m <= 0) return RT_OK;
+    hipLaunchKernelGGL(rt_screen_ends_kernel, dim3((unsigned)m), dim3(kScreenMaxWindow), 0, (hipStream_t)stream, pix,
+                       jit, ends);
+    RT_HIP(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_fill_points(double* out, int n, const double p[3], void* stream) {
+    if (n <= 0) return RT_OK;
+    hipLaunchKernelGGL(rt_fill_points_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       out, n, p[0], p[1], p[2]);
+    RT_HIP(hipGetLastError());
+    return RT_OK;
+}
+
 extern "C" int rt_probe_math_dev(int op, const double* in, int n, double* out, void* stream) {
     if (op != 0 && op != 1) return rt_fail(RT_EINVAL, "rt_probe_math_dev: unknown op");
     if (n < 0 || (n > 0 && (!in || !out))) return rt_fail(RT_EINVAL, "rt_probe_math_dev: bad buffers");

@@ -6,13 +6,15 @@
 // (randomUnit, :1148-1169), so where pixel p's samples sit in the rand() stream depends on the sample
 // counts of all earlier pixels.  The expensive part — one rayTraceRay per sample — is independent once
 // that position is known.  So:
-//   * the host predicts each pixel's sample count (the last resolved count: long runs of 16 inside
-//     objects, of 2 in converged background), builds the jittered rays of a chunk of pixels from the
-//     predicted stream positions and has the GPU trace them (rt_trace_rays_dev, the bit-exact
-//     rayTraceRay);
-//   * it then walks the chunk in order with the reference's own convergence arithmetic (FP64, same
-//     operation order, -ffp-contract=off).  At the first pixel whose count differs from the prediction
-//     the rest of the chunk used wrong stream positions: it is dropped and the next chunk starts there.
+//   * the host predicts each pixel's sample count (from the resolved pixel below it, else the last resolved
+//     pixel: counts are 2 in converged background and 16 on objects), which places every pixel of a chunk at
+//     a predicted stream position; the GPU forms the jittered rays of a window of stream positions around
+//     each prediction from the chunk's randomUnit() values and traces them (rt_trace_rays_dev, the
+//     bit-exact rayTraceRay);
+//   * the host then walks the chunk in order with the reference's own convergence arithmetic (FP64, same
+//     operation order, -ffp-contract=off), reading each sample's colour at its actual stream position.  When
+//     the actual position leaves a pixel's window the rest of the chunk is dropped and the next chunk starts
+//     there.
 // The result is the reference's frame bit for bit (tests: oracle_render_screen, and the reference's own
 // rand() consumption, tests/golden/screen.json).
 #include <hip/hip_runtime_api.h>
@@ -163,42 +165,51 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     const V3 up = normalize(cross(right, lookDirection));            // :1276-1277
     V3 walk = (lookAt + (double)cam->bottom_x * right) + (double)cam->bottom_y * up;   // :1279
 
-    // A chunk's ray ends and colours live in mapped, coherent pinned host memory that the trace kernel
-    // reads and writes directly: a round trip is one launch and one synchronisation, no copies.
-    const int kMaxRays = 1 << 16, kMaxPix = 4096;
-    DevBuf d_start;
-    HostBuf h_end, h_rgb;
-    void* d_end = nullptr;
+    // Speculation with windows (r03).  Each pixel's sample count is predicted from the pixel below it (its
+    // row is resolved; object edges move little from row to row) or, in the first row, from the last resolved
+    // pixel, which gives every pixel of a chunk a predicted first stream index.  The GPU traces, for every
+    // pixel, the samples of a window of kWin stream indices either side of its predicted range, so the chunk
+    // keeps resolving while the actual stream position drifts by up to kWin from the prediction (a count that
+    // differs at an object edge no longer ends the chunk).  The jittered rays are formed on the device from the
+    // chunk's randomUnit() values (rt_screen_form_ends): the host generates each stream value once and sends
+    // 24 bytes per value instead of the rays.  Simulated on the reference's own sample counts (demo frame):
+    // 759 round trips instead of 2,515, for ~85 traced samples per pixel instead of 7.
+    const int kMaxRays = 1 << 19, kMaxPix = 4096, kWin = 28;
+    const int kMaxJit = kMaxPix * 16 + 2 * kWin + 16;
+    static_assert(16 + 2 * kWin <= kScreenMaxWindow, "window exceeds the ray-formation workgroup");
+    DevBuf d_start, d_end;
+    HostBuf h_rgb, h_pix, h_jit;
     void* d_rgb = nullptr;
+    void* d_pix = nullptr;
+    void* d_jit = nullptr;
     Stream st;
     const size_t ray_bytes = (size_t)kMaxRays * 3 * sizeof(double);
     const unsigned mapped = hipHostMallocMapped | hipHostMallocCoherent;
     hipError_t e = hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&d_start.p, ray_bytes);
-    if (e == hipSuccess) e = hipHostMalloc(&h_end.p, ray_bytes, mapped);
+    if (e == hipSuccess) e = hipMalloc(&d_end.p, ray_bytes);
     if (e == hipSuccess) e = hipHostMalloc(&h_rgb.p, ray_bytes, mapped);
-    if (e == hipSuccess) e = hipHostGetDevicePointer(&d_end, h_end.p, 0);
+    if (e == hipSuccess) e = hipHostMalloc(&h_pix.p, (size_t)kMaxPix * sizeof(ScreenPix), mapped);
+    if (e == hipSuccess) e = hipHostMalloc(&h_jit.p, (size_t)kMaxJit * 3 * sizeof(double), mapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer(&d_rgb, h_rgb.p, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&d_pix, h_pix.p, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&d_jit, h_jit.p, 0);
     if (e != hipSuccess) return rt_fail(RT_ENOMEM, std::string("rt_render_screen: ") + hipGetErrorString(e));
-    {
-        std::vector<double> starts((size_t)kMaxRays * 3);
-        for (int k = 0; k < kMaxRays; ++k) {
-            starts[3 * k] = camera.x, starts[3 * k + 1] = camera.y, starts[3 * k + 2] = camera.z;
-        }
-        e = hipMemcpy(d_start.p, starts.data(), ray_bytes, hipMemcpyHostToDevice);
-        if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(e));
-    }
-    double* he = static_cast<double*>(h_end.p);
+    const double cam_p[3] = {camera.x, camera.y, camera.z};
+    rc = rt_fill_points(static_cast<double*>(d_start.p), kMaxRays, cam_p, st.s);
+    if (rc) return rc;
     const double* hr = static_cast<const double*>(h_rgb.p);
+    ScreenPix* hp = static_cast<ScreenPix*>(h_pix.p);
+    double* hj = static_cast<double*>(h_jit.p);
 
     Jitter jit(rand_kind, seed);
     V3 avgColor = v3(0.0, 0.0, 0.0);                                 // :1283, carried across pixels
     const long long P = (long long)W * H;
     long long p = 0;                                                 // first unresolved pixel (raster order)
     uint64_t S = 0;                                                  // its first sample in the stream
-    int predict = 16, chunk = 64;
+    int chunk = 64;
+    std::vector<uint8_t> counts((size_t)P, 0);                       // resolved sample counts (predictions)
     std::vector<V3> sp(kMaxPix);
-    std::vector<int> first(kMaxPix + 1);
     // RT_SCREEN_PROFILE=1: host build / GPU round trip / resolve times and chunk counts on stderr.
     const bool prof = getenv("RT_SCREEN_PROFILE") != nullptr;
     using clk = std::chrono::steady_clock;
@@ -206,42 +217,63 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     long long n_chunks = 0, n_rays = 0;
     while (p < P) {
         const auto c0 = clk::now();
-        // Chunk: pixels p .. p+m-1, `predict` samples each.
-        const int m = (int)std::min<long long>(std::min(chunk, kMaxRays / predict), P - p);
+        // Chunk: pixels p .. p+m-1 with their predicted counts and sample windows.
+        int m = (int)std::min<long long>(chunk, P - p);
         V3 w = walk;
-        int nr = 0;
+        int total = 0, jmax = 0;
+        long long spred = 0;                                         // predicted first sample, relative to S
         for (int q = 0; q < m; ++q) {
-            sp[q] = w;
-            first[q] = nr;
-            for (int k = 0; k < predict; ++k, ++nr) {
-                const V3 end = sp[q] + .5 * jit.at(S + (uint64_t)nr);   // ray.set(camera, screenPt + .5*randomUnit()) (:1296)
-                he[3 * nr] = end.x, he[3 * nr + 1] = end.y, he[3 * nr + 2] = end.z;
-            }
             const long long pix = p + q;
+            const int pred = (pix - W >= 0 && pix - W < p) ? counts[pix - W] : (p > 0 ? counts[p - 1] : 16);
+            const long long lo = std::max(0LL, spred - kWin), hi = spred + pred + kWin;
+            const int len = (int)(hi - lo);
+            if (total + len > kMaxRays || hi > kMaxJit) {
+                m = q;
+                break;
+            }
+            sp[q] = w;
+            hp[q].sp[0] = w.x, hp[q].sp[1] = w.y, hp[q].sp[2] = w.z;
+            hp[q].base = (int32_t)lo, hp[q].len = len, hp[q].off = total, hp[q].pad = 0;
+            total += len;
+            jmax = std::max(jmax, (int)hi);
+            spred += pred;
             w = w + right;                                           // screenPt += right (:1315)
             if ((int)(pix % W) == W - 1) w = (w - rightOffset) + up; // :1320-1321
         }
-        first[m] = nr;
+        for (int k = 0; k < jmax; ++k) {                             // randomUnit() values S .. S + jmax - 1
+            const V3& v = jit.at(S + (uint64_t)k);
+            hj[3 * k] = v.x, hj[3 * k + 1] = v.y, hj[3 * k + 2] = v.z;
+        }
         const auto c1 = clk::now();
-        // One round trip: the kernel reads the ends from and writes the colours to host memory.
-        rc = rt_trace_rays_dev(ctx, static_cast<const double*>(d_start.p), static_cast<const double*>(d_end), nr,
+        // One round trip: form the rays, trace them (colours straight into host memory), synchronise.
+        rc = rt_screen_form_ends(static_cast<const ScreenPix*>(d_pix), m, static_cast<const double*>(d_jit),
+                                 static_cast<double*>(d_end.p), st.s);
+        if (rc) return rc;
+        rc = rt_trace_rays_dev(ctx, static_cast<const double*>(d_start.p), static_cast<const double*>(d_end.p), total,
                                depth, static_cast<double*>(d_rgb), nullptr, st.s);
         if (rc) return rc;
         e = hipStreamSynchronize(st.s);
         if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(e));
 
         const auto c2 = clk::now();
-        // Resolve in order with the reference's loop (:1294-1311).
+        // Resolve in order with the reference's loop (:1294-1311), each sample read from its pixel's window.
         int q = 0;
+        long long A = 0;                                             // actual first sample of pixel q, relative to S
         bool broke = false;
-        for (; q < m && !broke; ++q) {
+        for (; q < m; ++q) {
+            const ScreenPix& X = hp[q];
+            if (A < X.base) {                                        // the stream ran behind the window
+                broke = true;
+                break;
+            }
             const V3 a0 = avgColor;
             double k;
             int n = 0;
             bool need_more = false;
             for (k = 0.0; k < kSamples; k++) {
-                if (n == predict) { need_more = true; break; }
-                const double* c = hr + 3 * (first[q] + n);
+                const long long idx = A + n - X.base;
+                if (idx >= X.len) { need_more = true; break; }       // ... or ran past it
+                const double* c = hr + 3 * (X.off + idx);
                 ++n;
                 const V3 color = v3(c[0], c[1], c[2]);
                 const V3 oldWeightedColor = (k + 1.0) * avgColor;
@@ -249,9 +281,8 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
                 const V3 weightedColor = k * avgColor;
                 if (length(weightedColor - oldWeightedColor) < small * k * (k + 1)) break;
             }
-            if (need_more) {                                         // more samples than predicted
+            if (need_more) {
                 avgColor = a0;
-                predict = 16;
                 broke = true;
                 break;
             }
@@ -265,15 +296,14 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
                 rgba8[4 * pix + 2] = to_u8(avgColor.z), rgba8[4 * pix + 3] = 255;
             }
             if (samples) samples[pix] = (uint8_t)n;
-            S += (uint64_t)n;
+            counts[pix] = (uint8_t)n;
+            A += n;
             walk = sp[q] + right;
             if ((int)(pix % W) == W - 1) walk = (walk - rightOffset) + up;
-            if (n != predict) {                                      // fewer samples than predicted
-                predict = n;
-                broke = true;
-            }
         }
+        // (q >= 1: pixel p's window starts at its own first sample and holds >= 16 + kWin samples)
         p += q;
+        S += (uint64_t)A;
         jit.consume_until(S);
         chunk = broke ? std::max(16, chunk / 2) : std::min(kMaxPix, chunk * 2);
         if (prof) {
@@ -282,7 +312,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
             t_gpu += std::chrono::duration<double>(c2 - c1).count();
             t_res += std::chrono::duration<double>(c3 - c2).count();
             ++n_chunks;
-            n_rays += nr;
+            n_rays += total;
         }
     }
     if (prof)

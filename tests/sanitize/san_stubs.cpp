@@ -88,3 +88,22 @@ extern "C" int rt_trace_rays_dev(rt_ctx* c, const double* starts, const double* 
     if (!c) return rt_fail(RT_EINVAL, "rt_trace_rays_dev: null context");
     return oracle_trace_rays(&c->scene, starts, ends, n, depth, rgb64f, raycount, 1);
 }
+// rt_render_screen's device-side ray formation (rt_kernel.hip), restated on the host with the same operations.
+int rt_screen_form_ends(const ScreenPix* pix, int m, const double* jit, double* ends, void*) {
+    for (int q = 0; q < m; ++q) {
+        const ScreenPix& P = pix[q];
+        if (P.len < 0 || P.len > kScreenMaxWindow) return rt_fail(RT_EINVAL, "rt_screen_form_ends: bad window");
+        for (int j = 0; j < P.len; ++j) {
+            const double* J = jit + 3 * (size_t)(P.base + j);
+            double* e = ends + 3 * (size_t)(P.off + j);
+            e[0] = P.sp[0] + 0.5 * J[0];
+            e[1] = P.sp[1] + 0.5 * J[1];
+            e[2] = P.sp[2] + 0.5 * J[2];
+        }
+    }
+    return RT_OK;
+}
+int rt_fill_points(double* out, int n, const double p[3], void*) {
+    for (int k = 0; k < n; ++k) out[3 * k] = p[0], out[3 * k + 1] = p[1], out[3 * k + 2] = p[2];
+    return RT_OK;
+}
