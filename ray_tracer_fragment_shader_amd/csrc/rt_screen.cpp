@@ -252,6 +252,9 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         rc = rt_trace_rays_dev(ctx, static_cast<const double*>(d_start.p), static_cast<const double*>(d_end.p), total,
                                depth, static_cast<double*>(d_rgb), nullptr, st.s);
         if (rc) return rc;
+        // While the GPU traces: generate the stream values the next chunk will need (rand() + normalize are
+        // the host's largest share of a round trip), so its build only copies them.
+        (void)jit.at(S + 2 * (uint64_t)jmax + 64);
         e = hipStreamSynchronize(st.s);
         if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(e));
 
