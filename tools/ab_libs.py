@@ -9,6 +9,7 @@ usage: ab_libs.py [c2,c3,c5] [rounds]        prints one JSON line per (config, l
 import ctypes
 import glob
 import json
+import math
 import os
 import shutil
 import statistics
@@ -38,6 +39,7 @@ def main():
     cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c2", "c3", "c5"]
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 9
     reps = int(os.environ.get("REPS", "20"))
+    moving = os.environ.get("MOVING", "0") == "1"      # a new eye every render (16-view orbit, as bench.py's leg)
     tmp = tempfile.mkdtemp()
     libs = {"base": load(abi.LIB_PATH, tmp, "base")}
     for d in sorted(glob.glob(os.path.join(ROOT, "tools", "_var", "*", "librt_amd.so"))):
@@ -58,20 +60,27 @@ def main():
         for c in cfgs:
             cfg = scenes.CONFIGS[c]
             sa = cfg.scene().to_abi()
-            cam = cfg.camera()
+            cams = [cfg.camera()]
+            if moving:
+                cams = []
+                for v in range(16):
+                    cm = cfg.camera()
+                    ang = 2.0 * math.pi * v / 16
+                    cm.eye = abi.vec3((60.0 * math.sin(ang), 100.0 + 10.0 * math.cos(ang), 200.0))
+                    cams.append(cm)
             b32, b8 = bufs[c]
             for name, L in libs.items():
                 abi.check(L.rt_set_scene(ctxs[name], ctypes.byref(sa)), "rt_set_scene")
-                la = (ctxs[name], ctypes.byref(cam), cfg.width, cfg.height, cfg.depth, None,
-                      ctypes.c_void_p(b32.data_ptr()), ctypes.c_void_p(b8.data_ptr()), None, None,
-                      ctypes.c_void_p(st.cuda_stream))
-                for _ in range(3 if r else 40):
-                    abi.check(L.rt_render_dev(*la), "rt_render_dev")
+                las = [(ctxs[name], ctypes.byref(cam), cfg.width, cfg.height, cfg.depth, None,
+                        ctypes.c_void_p(b32.data_ptr()), ctypes.c_void_p(b8.data_ptr()), None, None,
+                        ctypes.c_void_p(st.cuda_stream)) for cam in cams]
+                for i in range(3 if r else 40):
+                    abi.check(L.rt_render_dev(*las[i % len(las)]), "rt_render_dev")
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-                for _ in range(reps):
-                    L.rt_render_dev(*la)
+                for i in range(reps):
+                    L.rt_render_dev(*las[i % len(las)])
                 e1.record()
                 torch.cuda.synchronize()
                 if r:
