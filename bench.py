@@ -269,6 +269,11 @@ def dropin_binding_legs(W, H, B, cfg, frames=30):
 
 def main() -> int:
     args = parse()
+    # The JSON line goes to the process's original stdout; whatever native libraries write to fd 1 (RCCL prints
+    # its version banner there at communicator init) is sent to stderr, so stdout carries exactly one line.
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -621,7 +626,7 @@ def main() -> int:
         def c4_timeout():
             if rank == 0:
                 res_extra["c4"] = {"error": f"c4 leg did not finish within {args.c4_timeout:g} s"}
-                print(json.dumps(result()), flush=True)
+                print(json.dumps(result()), file=out, flush=True)
             os._exit(0)
 
         dog = threading.Timer(args.c4_timeout, c4_timeout)
@@ -781,7 +786,7 @@ def main() -> int:
                 "one_thread_value": round(per_core, 3),
                 "all_affinity_cores_linear_estimate": round(per_core * affinity_cores(), 3),
             }
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=out, flush=True)
     tr.close()
     if world > 1:
         dist.destroy_process_group()
