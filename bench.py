@@ -44,7 +44,7 @@ FP64_FLOPS_PER_FRAME = {"c1": 71.4e6, "c2": 1.038e9, "c3": 5.417e9, "c4": 5.417e
 BYTES_PER_PIXEL = 16 + 4       # RGBA32F framebuffer + RGBA8 display image written per pixel
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -71,7 +71,115 @@ def parse():
     ap.add_argument("--settle", type=float, default=0.25,
                     help="seconds of untimed back-to-back frames before the warm-up steps, so the GPU clock reaches "
                          "its loaded steady state (MI355X_MICROARCH.md 'DVFS give-back')")
-    return ap.parse_args()
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="print how this command would run (one process, or the per-rank child commands of "
+                         "--gpus N without a launcher) and exit without touching the GPU")
+    return ap.parse_args(argv)
+
+
+# ---- launch decision ---------------------------------------------------------------------------------------------
+# `--gpus N` is authoritative.  Under a launcher (torch.distributed.run sets WORLD_SIZE) the world size must equal
+# N.  Without one, N > 1 makes this process a launcher itself: it starts N fresh child ranks (one process per GPU,
+# the same RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* environment torch.distributed.run gives them), relays rank 0's
+# JSON line and exits with the worst child exit code.  The parent never initialises HIP (device counting through
+# torch.cuda.device_count() does not, on this image).
+
+def launch_plan(args, env, argv, device_count=None):
+    """("run", world) — bench in this process; ("launch", [(env, cmd), ...]) — start these child ranks;
+    ("error", message) — refuse.  `device_count` (callable) is consulted only for an nccl self-launch."""
+    ws = env.get("WORLD_SIZE")
+    if args.gpus < 1:
+        return "error", f"--gpus must be >= 1 (got {args.gpus})"
+    if ws is not None:
+        try:
+            w = int(ws)
+        except ValueError:
+            return "error", f"WORLD_SIZE={ws!r} is not an integer"
+        if w != args.gpus:
+            return "error", (f"WORLD_SIZE={w} (from the launcher) but --gpus {args.gpus}: the job would not measure "
+                             f"the GPU count it claims; launch {args.gpus} rank(s) or pass --gpus {w}")
+        return "run", w
+    if args.gpus == 1:
+        return "run", 1
+    n = args.gpus
+    if args.backend == "nccl" and device_count is not None:
+        have = device_count()
+        if have < n:
+            return "error", (f"--gpus {n} with the nccl (RCCL) backend needs {n} GPUs, this host shows {have}; "
+                             f"rehearse the N>1 path on fewer GPUs with --backend gloo")
+    port = env.get("MASTER_PORT") or str(free_port())
+    child_argv = [a for a in argv if a != "--dry-launch"]
+    ranks = []
+    for r in range(n):
+        e = {"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+             "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port}
+        ranks.append((e, [sys.executable, os.path.abspath(__file__)] + child_argv))
+    return "launch", ranks
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(ranks, out, grace_s=60.0) -> int:
+    """Start the child ranks, relay rank 0's JSON line to `out`, return the worst exit code.  A rank that fails
+    leaves the others `grace_s` seconds to finish (a peer blocked in a collective never would); then they are
+    terminated (exact PIDs) and counted as failed."""
+    import subprocess
+    import threading
+
+    procs = []
+    for e, cmd in ranks:
+        env = dict(os.environ)
+        env.update(e)
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if e["RANK"] == "0" else subprocess.DEVNULL,
+                                      stderr=None, text=True))
+    lines = []
+
+    def pump():
+        for line in procs[0].stdout:
+            s = line.strip()
+            if s.startswith("{") and '"metric"' in s:
+                lines.append(s)
+            elif s:
+                print(s, file=sys.stderr, flush=True)
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    first_fail = None
+    while True:
+        codes = [p.poll() for p in procs]
+        if all(c is not None for c in codes):
+            break
+        if first_fail is None and any(c not in (None, 0) for c in codes):
+            first_fail = time.monotonic()
+        if first_fail is not None and time.monotonic() - first_fail > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    print(f"bench.py: terminating rank pid {p.pid} (a peer failed {grace_s:g} s ago)", file=sys.stderr)
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=15)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        time.sleep(0.05)
+    th.join(timeout=10)
+    codes = [p.returncode for p in procs]
+    for r, c in enumerate(codes):
+        if c:
+            print(f"bench.py: rank {r} exited with {c}", file=sys.stderr)
+    worst = max(codes, key=lambda c: (c != 0, abs(c))) if codes else 1
+    if lines:
+        print(lines[-1], file=out, flush=True)
+    elif worst == 0:
+        print("bench.py: rank 0 printed no JSON line", file=sys.stderr)
+        worst = 1
+    return 128 - worst if worst < 0 else worst         # killed by signal k: 128 + k, as a shell reports it
 
 
 def affinity_cores() -> int:
@@ -267,14 +375,33 @@ def dropin_binding_legs(W, H, B, cfg, frames=30):
     return res
 
 
+def torch_device_count() -> int:
+    import torch
+    return torch.cuda.device_count()                   # counts devices without initialising HIP (this image)
+
+
 def main() -> int:
-    args = parse()
+    argv = sys.argv[1:]
+    args = parse(argv)
+    kind, plan_or_msg = launch_plan(args, os.environ, argv, device_count=torch_device_count)
+    if kind == "error":
+        print(f"bench.py: {plan_or_msg}", file=sys.stderr)
+        return 2
+    if args.dry_launch:
+        if kind == "run":
+            print(json.dumps({"launch": "in-process", "world_size": plan_or_msg}))
+        else:
+            print(json.dumps({"launch": "children", "world_size": len(plan_or_msg),
+                              "ranks": [{"env": e, "cmd": c} for e, c in plan_or_msg]}))
+        return 0
+    if kind == "launch":
+        return run_ranks(plan_or_msg, sys.stdout)
     # The JSON line goes to the process's original stdout; whatever native libraries write to fd 1 (RCCL prints
     # its version banner there at communicator init) is sent to stderr, so stdout carries exactly one line.
     sys.stdout.flush()
     out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = plan_or_msg
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -291,7 +418,12 @@ def main() -> int:
     if not torch.cuda.is_available():
         print("bench.py needs a HIP GPU", file=sys.stderr)
         return 2
-    rehearsal = args.backend == "gloo" and torch.cuda.device_count() == 1
+    ndev = torch.cuda.device_count()
+    if world > 1 and args.backend == "nccl" and ndev < world:
+        print(f"bench.py: {world} ranks with the nccl (RCCL) backend need {world} GPUs, this host shows {ndev} "
+              f"(rehearse with --backend gloo)", file=sys.stderr)
+        return 2
+    rehearsal = args.backend == "gloo" and ndev == 1
     if rehearsal:
         local = 0                                           # rehearsal: all ranks share the one GPU
     torch.cuda.set_device(local)
@@ -314,6 +446,13 @@ def main() -> int:
         t = torch.tensor([x], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
+
+    def fail_together(msg):
+        """Every rank reaches this with its own msg (None: fine); if any rank failed, all exit non-zero together
+        (one rank leaving alone would leave its peers blocked in the next collective)."""
+        bad = 0.0 if msg is None else 1.0
+        if max_over_ranks(bad) > 0.0:
+            raise SystemExit(msg or f"parity failure on another rank (this is rank {rank})")
 
     def frame_rays(tr, cam, W, H, B):
         b = tr.render(cam, W, H, B, rgba32f=False, raycount=True)
@@ -393,7 +532,8 @@ def main() -> int:
                 "phases_ms_max_over_ranks": phases_max,
                 "phases_note": "HIP events on each rank's render / comm streams over min(steps, 32) untimed frames: "
                                "render = rt_render_dev of the rank's bands; gather = from the rank's render end to its "
-                               "ncclSend done (rank > 0) or every ncclRecv done (rank 0; includes waiting for peers); "
+                               "ncclSend done (rank > 0), or from the frame's hand-off to every ncclRecv done (rank 0: "
+                               "its receives are posted without waiting for its own render; includes waiting for peers); "
                                "assemble = rank 0's unshuffle + expand into RGBA8; frame = rank 0 render start to "
                                "assembled image (frames overlap: double-buffered slabs)"}
         if parity is False:
@@ -432,8 +572,8 @@ def main() -> int:
         torch.cuda.synchronize()
         avg_kern_ms = kern_serial_ms = e[0].elapsed_time(e[1]) / 20
         nfly = 1
-        if rank == 0 and not info["parity"]:
-            raise SystemExit("parity failure: the gathered RGBA8 frame differs from the one-launch frame")
+        fail_together("parity failure: the gathered RGBA8 frame differs from the one-launch frame"
+                      if rank == 0 and not info["parity"] else None)
         parity = f"gathered RGBA8 frame == one-launch frame: {info['parity']}"
         res_extra["group"] = info
     else:
@@ -457,12 +597,11 @@ def main() -> int:
             rc = chk["raycount"].cpu().numpy().view(np.uint32)
             rays_frame = int((rc & 0xFFFF).sum()) + int((rc >> 16).sum())
             pinned = scenes.PINNED_RAYS.get(args.config)
-            if pinned is not None and rays_frame != pinned:
-                raise SystemExit(f"ray count {rays_frame} != reference {pinned}")
             g = np.load(os.path.join(ROOT, "tests", "golden", f"frames_{args.config}.npz"))
             got = chk["rgb64f"].cpu().numpy()[g["pj"], g["pi"]]
-            if not np.array_equal(got, g["samples"]):
-                raise SystemExit(f"parity failure: max err {np.abs(got - g['samples']).max()}")
+            fail_together(f"ray count {rays_frame} != reference {pinned}" if pinned is not None and rays_frame != pinned
+                          else None if np.array_equal(got, g["samples"]) else
+                          f"parity failure: max err {np.abs(got - g['samples']).max()}")
             parity = "bit-exact on 4096 sampled pixels vs the reference's rayTraceRay (tests/golden)"
             del chk, rc
 
@@ -620,14 +759,15 @@ def main() -> int:
     if extra_ok and not args.no_c4 and not strong and not rehearsal:
         # Guarded: the timed metric above is already final.  A failure of this leg is reported in its
         # entry; a leg that does not finish within --c4-timeout seconds (e.g. a peer that never joins the
-        # RCCL gather) ends the job with the line as it stands rather than leaving it without one.
+        # RCCL gather) ends the job with the line as it stands rather than leaving it without one, and with
+        # exit code 3, so the hang is not read as success.
         import threading
 
         def c4_timeout():
             if rank == 0:
                 res_extra["c4"] = {"error": f"c4 leg did not finish within {args.c4_timeout:g} s"}
                 print(json.dumps(result()), file=out, flush=True)
-            os._exit(0)
+            os._exit(3)                                     # the line stands, the job did not finish: non-zero
 
         dog = threading.Timer(args.c4_timeout, c4_timeout)
         dog.daemon = True

@@ -332,7 +332,9 @@ int rt_group_info(const rt_group* group, int* n_ranks, int* n_local, int* first_
  * What travels (the wire formats, rt_group_stats): for an achromatic scene (rt_scene_achromatic, decided by
  * each rank from its own context's scene — they are the same scene) GRAY8 for RGBA8 and GRAY32F for RGBA32F,
  * otherwise RGB8 and RGBA32F; rank 0 expands them into its images (rt_unpack_dev), byte for byte the images a
- * single rt_render_dev writes. */
+ * single rt_render_dev writes.  Every rank changes its scene (rt_set_scene) between the same frames; in a
+ * one-process-per-GPU group the first frame after a rank's scene changed all-reduces a fingerprint of the
+ * scene over the group (blocking, once per scene) and fails with RT_EINVAL on every rank when they differ. */
 int rt_render_multi(rt_group* group, const rt_camera* cam, int width, int height, int depth, int band_height,
                     int outputs, float* rgba32f, uint8_t* rgba8, void* stream);
 /* Wait for the group's own render and gather streams (e.g. before timing on a rank > 0). */

@@ -9,9 +9,12 @@
 //
 //   render stream rs_r:  wait sent[r][b] -> rt_render_dev(rows of r) into slab[r][b] -> record rendered[r][b]
 //   comm stream   cs_r:  wait rendered[r][b] -> ncclSend(slab[r][b] -> rank 0)      -> record sent[r][b]
-//   root cs_0:           wait rendered[b] -> ncclRecv(gathered[b] + q*slab <- q), q = 1..n-1; wait the caller
-//                        stream's earlier work (received[b]) -> unshuffle(gathered[b] + root slab[b] -> image)
+//   root cs_0:           ncclRecv(gathered[b] + q*slab <- q), q = 1..n-1 (posted at once: they do not wait for
+//                        the root's own render); wait the caller stream's earlier work (received[b]) and the
+//                        root's render (rendered[b]) -> unshuffle(gathered[b] + root slab[b] -> image)
 //                        -> record assembled[b]; the caller's stream waits for assembled[b]
+// A process's ranks must switch scenes between the same frames: one-process-per-GPU groups agree on the scene
+// (hence the wire formats) with a small all-reduce whenever a rank's scene changes (agree_on_scene).
 // Stream priorities: rs lowest, cs highest (the gather's kernels do not queue behind the next render grid).
 // A one-rank group renders straight into the caller's image on the caller's stream (identity band plan).
 //
@@ -61,6 +64,9 @@ struct Rank {
     void* slab[2][kKinds] = {{nullptr, nullptr}, {nullptr, nullptr}};
     size_t slab_cap[2][kKinds] = {{0, 0}, {0, 0}};
     ncclComm_t comm = nullptr;
+    uint64_t* d_agree = nullptr;               // rt_group_create_rank: the scene agreement's all-reduce buffer
+    uint64_t agreed_gen = 0;                   // the context's scene generation the group last agreed on
+    bool agreed = false;
     PhaseEvents ph[kRing];
 };
 
@@ -83,6 +89,8 @@ struct rt_group {
     bool timing = false;
     uint64_t t_first = 0;
     int last_wire[kKinds] = {-1, -1};
+    // RT_GATHER_ROOT_WAITS=1 (A/B): the root's receives / peer copies wait for the root's own render first (r03)
+    bool root_waits = false;
     uint64_t last_payload = 0;
 };
 
@@ -160,6 +168,7 @@ extern "C" int rt_group_destroy(rt_group* g) {
     for (auto& r : g->ranks) {
         (void)hipSetDevice(r.device);
         if (r.comm) (void)ncclCommDestroy(r.comm);
+        if (r.d_agree) (void)hipFree(r.d_agree);
         for (auto& e : r.ph)
             for (hipEvent_t ev : {e.r0, e.r1, e.g0, e.g1, e.a1})
                 if (ev) (void)hipEventDestroy(ev);
@@ -209,6 +218,7 @@ extern "C" int rt_group_create(rt_ctx* const* ctxs, int n, int transport, rt_gro
     if (transport == RT_TRANSPORT_RCCL && !distinct)
         return rt_fail(RT_EINVAL, "rt_group_create: RCCL needs one context per device (use RT_TRANSPORT_COPY)");
     rt_group* g = new rt_group();
+    if (const char* e = getenv("RT_GATHER_ROOT_WAITS")) g->root_waits = atoi(e) != 0;
     g->n_ranks = n;
     g->transport = transport;
     g->owns_root = true;
@@ -249,6 +259,7 @@ extern "C" int rt_group_create_rank(rt_ctx* ctx, int n_ranks, int rank, const ui
     if (!ctx || !id || n_ranks <= 0 || rank < 0 || rank >= n_ranks)
         return rt_fail(RT_EINVAL, "rt_group_create_rank: bad arguments");
     rt_group* g = new rt_group();
+    if (const char* e = getenv("RT_GATHER_ROOT_WAITS")) g->root_waits = atoi(e) != 0;
     g->n_ranks = n_ranks;
     g->transport = RT_TRANSPORT_RCCL;
     g->owns_root = rank == 0;
@@ -357,6 +368,33 @@ extern "C" int rt_group_get_stats(rt_group* g, rt_group_stats* st) {
     return RT_OK;
 }
 
+// One process per GPU (rt_group_create_rank): each rank picks its wire formats from its own context's scene, so
+// the ranks must hold the same scene or the byte counts of ncclSend / ncclRecv disagree (a hang or a torn frame).
+// Whenever this rank's scene generation changed since the last agreement — every rank changes its scene between
+// the same frames (include/rt_api.h, rt_render_multi) — the group all-reduces (max) {h, ~h, a, ~a} of the scene
+// fingerprint h and the achromatic flag a: every rank then sees min = max for both, or fails with RT_EINVAL.
+int agree_on_scene(rt_group* g, Rank& r, int achro) {
+    uint64_t gen = 0, h = 0;
+    rt_ctx_scene_id(r.ctx, &gen, &h);
+    if (r.agreed && gen == r.agreed_gen) return RT_OK;
+    G_HIP(hipSetDevice(r.device));
+    if (!r.d_agree && hipMalloc(&r.d_agree, 4 * sizeof(uint64_t)) != hipSuccess)
+        return rt_fail(RT_ENOMEM, "rt_render_multi: hipMalloc of the scene agreement buffer failed");
+    const uint64_t a = (uint64_t)achro;
+    uint64_t v[4] = {h, ~h, a, ~a};
+    // on the comm stream, behind the previous frames' exchanges (collectives run in the same order on every rank)
+    G_HIP(hipMemcpyAsync(r.d_agree, v, sizeof(v), hipMemcpyHostToDevice, r.cs));
+    G_NCCL(ncclAllReduce(r.d_agree, r.d_agree, 4, ncclUint64, ncclMax, r.comm, r.cs));
+    G_HIP(hipMemcpyAsync(v, r.d_agree, sizeof(v), hipMemcpyDeviceToHost, r.cs));
+    G_HIP(hipStreamSynchronize(r.cs));
+    if (v[0] != ~v[1] || v[2] != ~v[3])
+        return rt_fail(RT_EINVAL, "rt_render_multi: the group's ranks hold different scenes (wire formats would "
+                                  "disagree); call rt_set_scene with the same scene on every rank");
+    r.agreed = true;
+    r.agreed_gen = gen;
+    return RT_OK;
+}
+
 extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, int depth, int band_height,
                                int outputs, float* rgba32f, uint8_t* rgba8, void* stream) {
     if (!g) return rt_fail(RT_EINVAL, "rt_render_multi: null group");
@@ -380,6 +418,9 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     for (auto& r : g->ranks)
         if (rt_ctx_achromatic(r.ctx) != achro)
             return rt_fail(RT_EINVAL, "rt_render_multi: the ranks' contexts hold different scenes");
+    // ... and across the processes of a one-process-per-GPU group
+    if (g->n_ranks > 1 && (int)g->ranks.size() < g->n_ranks && (rc = agree_on_scene(g, g->ranks[0], achro)))
+        return rc;
     const int wire[kKinds] = {achro ? RT_PIXEL_GRAY32F : RT_PIXEL_RGBA32F, achro ? RT_PIXEL_GRAY8 : RT_PIXEL_RGB8};
     size_t elem[kKinds];
     for (int k = 0; k < kKinds; ++k) {
@@ -491,7 +532,9 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         for (size_t q = 0; q < g->ranks.size(); ++q) {
             Rank& r = g->ranks[q];
             G_HIP(hipSetDevice(r.device));
-            G_HIP(hipStreamWaitEvent(r.cs, r.rendered[b], 0));
+            // a sender waits for its slab; the root's receives land in gathered[b], which does not depend on the
+            // root's own render: they are posted at once (the root's slab is waited for by the unpack below)
+            if (r.rank != 0 || g->root_waits) G_HIP(hipStreamWaitEvent(r.cs, r.rendered[b], 0));
             if (pe[q]) G_HIP(hipEventRecord(pe[q]->g0, r.cs));
         }
         G_NCCL(ncclGroupStart());
@@ -530,11 +573,12 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     } else {
         Rank& root = g->ranks[0];
         G_HIP(hipSetDevice(root.device));
-        // the root's gather: from its own render's end (as in RCCL mode) to the last peer copy
-        G_HIP(hipStreamWaitEvent(root.cs, root.rendered[b], 0));
+        // the root's gather: from the frame's hand-off to the last peer copy; each copy waits only for its own
+        // rank's render (the root's slab is waited for by the unpack below)
+        if (g->root_waits) G_HIP(hipStreamWaitEvent(root.cs, root.rendered[b], 0));
         if (pe[0]) G_HIP(hipEventRecord(pe[0]->g0, root.cs));
         for (auto& r : g->ranks) {
-            G_HIP(hipStreamWaitEvent(root.cs, r.rendered[b], 0));
+            if (r.rank != 0) G_HIP(hipStreamWaitEvent(root.cs, r.rendered[b], 0));
             for (int k = 0; k < kKinds; ++k) {
                 if (!kind_on[k] || r.rank == 0) continue;      // the root's own slab is unshuffled in place
                 char* dst = (char*)g->gathered[b][k] + (size_t)r.rank * slab_rows * W * elem[k];
@@ -558,6 +602,7 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         G_HIP(hipSetDevice(root.device));
         G_HIP(hipEventRecord(g->received[b], st));                   // caller's earlier work on the image
         G_HIP(hipStreamWaitEvent(root.cs, g->received[b], 0));
+        G_HIP(hipStreamWaitEvent(root.cs, root.rendered[b], 0));     // the root's own slab
         for (int k = 0; k < kKinds; ++k) {
             if (!kind_on[k]) continue;
             rc = rt_unpack_dev_ex(g->gathered[b][k], root.slab[b][k], outs[k], W, H, wire[k], kImageFormat[k], hb,

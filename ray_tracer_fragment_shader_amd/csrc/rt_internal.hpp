@@ -1,6 +1,8 @@
 // rt_internal.hpp — host-side helpers shared by rt_host.cpp and rt_kernel.hip (not part of the ABI).
 #pragma once
 
+#include <stdint.h>
+
 #include <string>
 #include <vector>
 
@@ -22,6 +24,11 @@ int rt_ctx_device(const rt_ctx* ctx);
 
 // 1 when the context's uploaded scene is achromatic (rt_scene_achromatic): GRAY pixel formats are exact.
 int rt_ctx_achromatic(const rt_ctx* ctx);
+
+// The context's scene generation (changes with every rt_set_scene that uploads a different scene) and a
+// fingerprint of the uploaded record (FNV-1a of the flattened scene): rt_group.cpp agrees on the scene — hence
+// on the wire formats — across the processes of a group whenever a rank's generation changes.
+void rt_ctx_scene_id(const rt_ctx* ctx, uint64_t* gen, uint64_t* fingerprint);
 
 // rt_unshuffle_dev with rank 0's rows read from `rank0_slab` instead of the gathered buffer (the group's root
 // unshuffles its own slab in place of sending it to itself); rank0_slab = nullptr: from `gathered`.

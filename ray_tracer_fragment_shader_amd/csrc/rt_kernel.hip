@@ -374,6 +374,7 @@ struct rt_ctx {
     // per call, pipelined 0.079 either way (tools/packed_probe.py).
     int copy_mode = 1;
     int copy_kernel = 1;                       // RT_COPY_KERNEL=0: hipMemcpyAsync for rt_host_alloc memory too (A/B)
+    int copy_blocks = 0;                       // RT_COPY_BLOCKS: workgroups of the copy kernel (0: one per 4 KB, <= 1024)
     // Adaptive tile-row order (rt_order_kernel): the first render of a new (scene, camera, size, rows,
     // depth, outputs) view uses the identity order; the second render of the same view is a calibration
     // render that also times its tile rows; later renders dispatch the rows by decreasing time.  A render
@@ -395,27 +396,43 @@ struct rt_ctx {
     // Primary cone masks of the calibrated view (scenes with >= kPrimaryConeMin spheres): the calibration render
     // writes each tile's mask (d_cone_tile), rt_cone_permute_kernel puts them in dispatch order (d_cone_disp),
     // and later renders of exactly that view (order_key) read them instead of recomputing them.  Renders of
-    // another camera compute their own.  d_cone_disp is rewritten only after the device has drained every
-    // render queued with it (cone_readers), whatever stream it went to.
+    // another camera compute their own.  One-wave (8 x 8 tile) variants only.  Ordering against renders on
+    // other streams: view_ev and the reader tracking below.
     uint64_t* d_cone_tile = nullptr;
     uint64_t* d_cone_disp = nullptr;
     size_t cone_cap = 0;                       // tiles each holds
     bool cone_valid = false;                   // d_cone_disp holds the masks of view order_key
-    bool cone_readers = false;                 // a render reading d_cone_disp was queued since the last drain
+    // Cross-stream ordering of the per-view state: the per-eye records inside d_scene (rt_prepare_kernel) and the
+    // calibration buffers (d_row_cost, d_tile_rows, d_cone_tile, d_cone_disp).  Every render reads the per-eye
+    // records; a render that prepares a new eye or calibrates also writes.  A writer records view_ev on its stream
+    // after its last write; a render on another stream first waits for view_ev on the GPU (read-after-write,
+    // write-after-write).  Renders are tracked by stream: a writer drains the device first when renders were queued
+    // on a stream other than its own since the last drain (write-after-read); same-stream renders are ordered by
+    // the stream, so one stream per context (the benchmark's layout) never waits or drains.
+    hipEvent_t view_ev = nullptr;
+    hipStream_t view_st = nullptr;
+    bool view_rec = false;                     // view_ev was recorded (on view_st)
+    hipStream_t reader_st = nullptr;           // the stream of the renders queued since the last drain ...
+    bool readers = false;                      // ... (any)
+    bool readers_multi = false;                // ... on more than one stream
     int cone_cache = RT_CONE_CACHE_DEFAULT;    // RT_CONE_CACHE=0: always compute the masks in the kernel (A/B)
     uint64_t scene_gen = 0;
+    uint64_t scene_hash = 0;                   // FNV-1a of `blob` (rt_ctx_scene_id)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // The host-buffer calls (rt_render, rt_render_packed, rt_render_packed_async) run on the context's own
     // streams: renders on `rs` (blocking w.r.t. the null stream, like the null-stream renders it replaced), the
     // device-to-host copies on `cs`, so an asynchronous frame's copy overlaps the next frame's render.
     hipStream_t rs = nullptr, cs = nullptr;
-    hipEvent_t rendered[2] = {nullptr, nullptr};   // slot b's packed frame is in its device buffer
-    hipEvent_t copied[2] = {nullptr, nullptr};     // slot b's packed frame is in its host buffer
-    bool copied_rec[2] = {false, false};
+    // rt_render_packed_async frame t uses slot t % kSlots (device buffer 5 + slot): up to kSlots - 1 frames of
+    // latency behind the one being queued
+    static constexpr int kSlots = 3;
+    hipEvent_t rendered[kSlots] = {};          // slot b's packed frame is in its device buffer
+    hipEvent_t copied[kSlots] = {};            // slot b's packed frame is in its host buffer
+    bool copied_rec[kSlots] = {};
     uint64_t ticket = 0;                       // rt_render_packed_async frames queued so far
     // rt_render's device buffers (grow-only, reused across calls): rgba32f, rgba8, rgb64f, raycount, sums,
     // packed slot 0, packed slot 1
-    static constexpr int kBufs = 7;
+    static constexpr int kBufs = 5 + kSlots;
     void* d_out[kBufs] = {};
     size_t out_cap[kBufs] = {};
 };
@@ -468,7 +485,8 @@ extern "C" int rt_ctx_destroy(rt_ctx* c) {
     if (c->d_cone_disp) (void)hipFree(c->d_cone_disp);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
-    for (int b = 0; b < 2; ++b) {
+    if (c->view_ev) (void)hipEventDestroy(c->view_ev);
+    for (int b = 0; b < rt_ctx::kSlots; ++b) {
         if (c->rendered[b]) (void)hipEventDestroy(c->rendered[b]);
         if (c->copied[b]) (void)hipEventDestroy(c->copied[b]);
     }
@@ -494,7 +512,8 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_MIN_WAVES")) c->min_waves = atoi(e);
     if (const char* e = getenv("RT_WG_STAGING")) c->wg_staging = atoi(e) != 0;
     if (const char* e = getenv("RT_TILE_ORDER")) c->order_mode = atoi(e) == 1 ? 1 : 0;   // 1: bottom-to-top (A/B)
-    if (const char* e = getenv("RT_COPY_MODE")) c->copy_mode = atoi(e) == 0 ? 0 : 1;
+    if (const char* e = getenv("RT_COPY_MODE")) c->copy_mode = std::min(std::max(atoi(e), 0), 2);
+    if (const char* e = getenv("RT_COPY_BLOCKS")) c->copy_blocks = std::max(atoi(e), 0);
     if (const char* e = getenv("RT_COPY_KERNEL")) c->copy_kernel = atoi(e) != 0;
     if (const char* e = getenv("RT_CONE_CACHE")) c->cone_cache = atoi(e) != 0;
     if (hipMalloc(&c->d_tile_rows, sizeof(int32_t) * kOrderMax) != hipSuccess ||
@@ -505,9 +524,10 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     c->n_tile_rows = kOrderMax;
     bool ok = hipMemset(c->d_tile_rows, 0, sizeof(int32_t) * kOrderMax) == hipSuccess &&
               hipEventCreate(&c->ev0) == hipSuccess && hipEventCreate(&c->ev1) == hipSuccess &&
+              hipEventCreateWithFlags(&c->view_ev, hipEventDisableTiming) == hipSuccess &&
               hipStreamCreateWithFlags(&c->rs, hipStreamDefault) == hipSuccess &&
               hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking) == hipSuccess;
-    for (int b = 0; b < 2 && ok; ++b)
+    for (int b = 0; b < rt_ctx::kSlots && ok; ++b)
         ok = hipEventCreateWithFlags(&c->rendered[b], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->copied[b], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
@@ -521,6 +541,11 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
 int rt_ctx_device(const rt_ctx* c) { return c ? c->device : -1; }
 
 int rt_ctx_achromatic(const rt_ctx* c) { return c && c->scene_set && c->achromatic ? 1 : 0; }
+
+void rt_ctx_scene_id(const rt_ctx* c, uint64_t* gen, uint64_t* fingerprint) {
+    *gen = c && c->scene_set ? c->scene_gen : 0;
+    *fingerprint = c && c->scene_set ? c->scene_hash : 0;
+}
 
 extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     if (!c) return rt_fail(RT_EINVAL, "rt_set_scene: null context");
@@ -561,6 +586,9 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     c->eye_valid = false;
     c->scene_set = true;
     c->blob.swap(blob);
+    uint64_t fp = 0xcbf29ce484222325ull;
+    for (unsigned char byte : c->blob) fp = (fp ^ byte) * 0x100000001b3ull;
+    c->scene_hash = fp;
     ++c->scene_gen;
     return RT_OK;
 }
@@ -692,38 +720,53 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
                                 memcmp(key.data() + kCam, c->order_key.data() + kCam, key.size() - kCam) == 0;
         if (c->order_valid && key == c->order_key) {
             P.tile_rows = c->d_tile_rows;
-            if (c->cone_valid) {
-                P.cone_in = c->d_cone_disp;
-                c->cone_readers = true;
-            }
+            // (the cached masks hold one mask per one-wave 8 x 8 tile: the 256-thread A/B variants never read them)
+            if (c->cone_valid && !big) P.cone_in = c->d_cone_disp;
         } else if (same_shape) {
             P.tile_rows = c->d_tile_rows;               // another camera: the last calibrated order
             if (++c->stale >= kRecalibrate) {           // ... re-timed every kRecalibrate-th render
-                RT_HIP(hipMemsetAsync(c->d_row_cost, 0, sizeof(uint32_t) * tiles_y, st));
                 P.row_cost = c->d_row_cost;
                 calibrate = true;
                 c->order_valid = false;
             }
         } else if (c->seen_valid && key == c->seen_key) {
-            RT_HIP(hipMemsetAsync(c->d_row_cost, 0, sizeof(uint32_t) * tiles_y, st));
             P.row_cost = c->d_row_cost;                 // calibration render (identity order)
             calibrate = true;
             c->order_valid = false;                     // rt_order_kernel rewrites d_tile_rows below
-            cone_calib = c->cone_cache && c->n_padded >= kPrimaryConeMin && !c->tree && !c->transparent;
+            // the calibration records one mask per tile from lane 0 of its wave: one-wave workgroups only
+            cone_calib = c->cone_cache && c->n_padded >= kPrimaryConeMin && !c->tree && !c->transparent && !big &&
+                         RT_WG_FAST == 64;
         } else {
             c->seen_key = key;                          // first render of this view: identity order
             c->seen_valid = true;
         }
     }
-    if (calibrate) c->cone_valid = false;
-    if (cone_calib) {
-        // this (static) view's calibration also records its cone masks; the buffers may still be read by
-        // renders queued earlier on any stream: drain the device first when one was
-        const size_t need = cone_slots((size_t)tiles_x * tiles_y);
-        if (c->cone_readers || need > c->cone_cap) {
-            RT_HIP(hipDeviceSynchronize());
-            c->cone_readers = false;
+    const bool prepare = capturing || c->ever_captured || !c->eye_valid || memcmp(c->eye, cam->eye, sizeof(c->eye)) != 0;
+    const size_t cone_need = cone_calib ? cone_slots((size_t)tiles_x * tiles_y) : 0;
+    if (!capturing) {                                   // (a captured render carries its own prepare launch)
+        // read-after-write / write-after-write: the last write of the view state was queued on another stream
+        if (c->view_rec && c->view_st != st) RT_HIP(hipStreamWaitEvent(st, c->view_ev, 0));
+        if (prepare || calibrate) {
+            // write-after-read: renders queued on other streams may still read what this render rewrites
+            if ((c->readers && (c->readers_multi || c->reader_st != st)) || cone_need > c->cone_cap)
+                RT_HIP(hipDeviceSynchronize());
+            c->readers = c->readers_multi = false;      // same-stream renders are ordered before the rewrite
         }
+        if (!c->readers) {                              // this render reads the view state on st
+            c->readers = true;
+            c->reader_st = st;
+        } else if (c->reader_st != st) {
+            c->readers_multi = true;
+        }
+    }
+    if (calibrate) {
+        c->cone_valid = false;
+        RT_HIP(hipMemsetAsync(c->d_row_cost, 0, sizeof(uint32_t) * tiles_y, st));
+    }
+    if (cone_calib) {
+        // this (static) view's calibration also records its cone masks (the device is drained above when the
+        // buffers must grow)
+        const size_t need = cone_slots((size_t)tiles_x * tiles_y);
         if (need > c->cone_cap) {
             if (c->d_cone_tile) (void)hipFree(c->d_cone_tile);
             if (c->d_cone_disp) (void)hipFree(c->d_cone_disp);
@@ -745,7 +788,7 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
     hipError_t e;
     // Primary-ray sphere data for this eye (stream-ordered; only when the eye changes, or always once graphs
     // that carry their own prepare launch exist).
-    if (capturing || c->ever_captured || !c->eye_valid || memcmp(c->eye, cam->eye, sizeof(c->eye)) != 0) {
+    if (prepare) {
         c->eye_valid = false;
         dim3 pg((unsigned)((std::max(c->n_padded, 1) + kThreads - 1) / kThreads));
         hipLaunchKernelGGL(rt_prepare_kernel, pg, dim3(kThreads), 0, st, c->d_scene, cam->eye[0], cam->eye[1],
@@ -815,6 +858,11 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
         c->cone_valid = cone_calib;
         c->stale = 0;
     }
+    if ((prepare || calibrate) && !capturing) {
+        RT_HIP(hipEventRecord(c->view_ev, st));         // later renders on other streams wait for these writes
+        c->view_st = st;
+        c->view_rec = true;
+    }
     return RT_OK;
 }
 
@@ -880,7 +928,8 @@ static int copy_to_host(rt_ctx* c, void* host, const void* dev, size_t bytes, hi
     if (!bytes) return RT_OK;
     void* dmap = pinned_device_ptr(host, bytes);
     if (dmap && c->copy_kernel && ((uintptr_t)dmap | (uintptr_t)dev) % 16 == 0) {
-        const unsigned blocks = (unsigned)std::min<size_t>((bytes / 16 + kThreads - 1) / kThreads + 1, 1024);
+        unsigned blocks = (unsigned)std::min<size_t>((bytes / 16 + kThreads - 1) / kThreads + 1, 1024);
+        if (c->copy_blocks > 0) blocks = std::min(blocks, (unsigned)c->copy_blocks);
         hipLaunchKernelGGL(rt_copy_out_kernel, dim3(blocks), dim3(kThreads), 0, st, (const uint8_t*)dev,
                            (uint8_t*)dmap, bytes);
         RT_HIP(hipGetLastError());
@@ -946,9 +995,13 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
     *npx_out = npx;
     void* px = nullptr;
     void* rcb = nullptr;
-    if ((rc = ctx_buffer(c, 5 + slot, npx * pb, &px))) return rc;
+    // RT_COPY_MODE=2 (A/B): the kernel stores the frame straight into the pinned host buffer (mapped into the
+    // device's address space), no device buffer and no copy
+    void* direct = c->copy_mode == 2 ? pinned_device_ptr(host, npx * pb) : nullptr;
+    if (direct) px = direct;
+    else if ((rc = ctx_buffer(c, 5 + slot, npx * pb, &px))) return rc;
     if (with_stats && ((rc = ctx_buffer(c, 3, npx * 4, &rcb)) || (rc = ctx_buffer(c, 4, 16, sums)))) return rc;
-    const hipStream_t cs = c->copy_mode == 1 ? c->rs : c->cs;
+    const hipStream_t cs = c->copy_mode != 0 ? c->rs : c->cs;
     // the slot's device buffer is free once its previous frame's copy has left (stream-ordered on the GPU)
     if (c->copied_rec[slot] && cs != c->rs) RT_HIP(hipStreamWaitEvent(c->rs, c->copied[slot], 0));
     if (with_stats) RT_HIP(hipEventRecord(c->ev0, c->rs));
@@ -963,7 +1016,7 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
         RT_HIP(hipEventRecord(c->rendered[slot], c->rs));
         RT_HIP(hipStreamWaitEvent(cs, c->rendered[slot], 0));
     }
-    if ((rc = copy_to_host(c, host, px, npx * pb, cs))) return rc;
+    if (!direct && (rc = copy_to_host(c, host, px, npx * pb, cs))) return rc;
     RT_HIP(hipEventRecord(c->copied[slot], cs));
     c->copied_rec[slot] = true;
     return RT_OK;
@@ -973,11 +1026,13 @@ extern "C" int rt_render_packed(rt_ctx* c, const rt_scene* scene, const rt_camer
                                 int format, void* host_pixels, rt_stats* stats) {
     size_t npx = 0;
     void* sums = nullptr;
-    if (c) c->ticket++;
-    int rc = render_packed_queue(c, scene, cam, W, H, depth, format, host_pixels, c ? (int)(c->ticket & 1) : 0,
-                                 stats != nullptr, &npx, &sums);
+    if (!c) return rt_fail(RT_EINVAL, "rt_render_packed: null context");
+    const uint64_t t = c->ticket + 1;                   // issued only once the frame is queued
+    int rc = render_packed_queue(c, scene, cam, W, H, depth, format, host_pixels, (int)(t % rt_ctx::kSlots), stats != nullptr,
+                                 &npx, &sums);
     if (rc) return rc;
-    RT_HIP(hipEventSynchronize(c->copied[c->ticket & 1]));
+    c->ticket = t;
+    RT_HIP(hipEventSynchronize(c->copied[t % rt_ctx::kSlots]));
     if (stats) {
         RT_HIP(hipStreamSynchronize(c->rs));
         return read_stats(c, npx, (const unsigned long long*)sums, stats);
@@ -991,7 +1046,8 @@ extern "C" int rt_render_packed_async(rt_ctx* c, const rt_scene* scene, const rt
     void* sums = nullptr;
     if (!c) return rt_fail(RT_EINVAL, "rt_render_packed_async: null context");
     const uint64_t t = c->ticket + 1;
-    int rc = render_packed_queue(c, scene, cam, W, H, depth, format, host_pixels, (int)(t & 1), false, &npx, &sums);
+    int rc = render_packed_queue(c, scene, cam, W, H, depth, format, host_pixels, (int)(t % rt_ctx::kSlots), false, &npx,
+                                 &sums);
     if (rc) return rc;
     c->ticket = t;
     if (ticket) *ticket = t;
@@ -1007,8 +1063,9 @@ extern "C" int rt_ctx_wait(rt_ctx* c, uint64_t ticket) {
         RT_HIP(hipStreamSynchronize(c->cs));
         return RT_OK;
     }
-    // slot (ticket & 1) holds this frame's copy or a later one's (which the GPU orders after it)
-    if (c->copied_rec[ticket & 1]) RT_HIP(hipEventSynchronize(c->copied[ticket & 1]));
+    // slot (ticket % kSlots) holds this frame's copy or a later one's (which the GPU orders after it)
+    const int sl = (int)(ticket % rt_ctx::kSlots);
+    if (c->copied_rec[sl]) RT_HIP(hipEventSynchronize(c->copied[sl]));
     return RT_OK;
 }
 

@@ -111,3 +111,43 @@ def test_view_change_with_renders_in_flight_on_other_streams(tr):
         assert torch.equal(b_frame["rgb64f"], ref)
     finally:
         fresh.close()
+
+
+@pytest.mark.parametrize("name", ["c2", "c3"])
+def test_calibrate_on_one_stream_read_on_another(name):
+    """The calibration render (and the order / mask-permute kernels after it) queued on s1, then at once — no
+    synchronisation — cached renders of the same view on s2 and s3: they must wait for the calibration's buffers
+    on the GPU (the context's calibration event), and every frame hashes to the reference.  Then a view change
+    calibrated on s2 while s3's cached renders may still be reading: A frames stay exact, B equals a fresh render."""
+    cfg = scenes.CONFIGS[name]
+    W, H = cfg.width, cfg.height
+    sc = cfg.scene()
+    want = golden.manifest()["frames"][name]["fnv1a64"]
+    t = Tracer(0)
+    try:
+        t.set_scene(sc)
+        s1, s2, s3 = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+        bufs = [t.alloc(W, H, rgba32f=False, rgb64f=True) for _ in range(6)]
+        t.render_into(cfg.camera(), W, H, cfg.depth, bufs[0], stream=s1)      # first render: identity order
+        torch.cuda.synchronize()
+        t.render_into(cfg.camera(), W, H, cfg.depth, bufs[1], stream=s1)      # calibration (not waited for)
+        t.render_into(cfg.camera(), W, H, cfg.depth, bufs[2], stream=s2)      # cached, another stream
+        t.render_into(cfg.camera(), W, H, cfg.depth, bufs[3], stream=s3)
+        t.render_into(cfg.camera(), W, H, cfg.depth, bufs[4], stream=s3)
+        vb = _moved(cfg, 0.7)
+        b0 = t.render(vb, W, H, cfg.depth, rgba32f=False, rgb64f=True, stream=s2)
+        b1 = t.render(vb, W, H, cfg.depth, rgba32f=False, rgb64f=True, stream=s2)    # calibrates B on s2
+        t.render_into(cfg.camera(), W, H, cfg.depth, bufs[5], stream=s1)
+        torch.cuda.synchronize()
+        for k, b in enumerate(bufs):
+            assert _hash(b) == want, f"A frame {k}"
+        fresh = Tracer(0)
+        try:
+            fresh.set_scene(sc)
+            ref = fresh.render(vb, W, H, cfg.depth, rgba32f=False, rgb64f=True)["rgb64f"]
+            torch.cuda.synchronize()
+            assert torch.equal(b0["rgb64f"], ref) and torch.equal(b1["rgb64f"], ref)
+        finally:
+            fresh.close()
+    finally:
+        t.close()
