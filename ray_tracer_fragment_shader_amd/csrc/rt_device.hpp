@@ -95,6 +95,10 @@
 // There they come with the continuation parked in LDS across the light loop (RT_PARK_ND): without it the
 // extra live state spilled 12 B/lane at 6 waves/SIMD (c2 HBM writes 1.01x -> 1.22x); with it no spills,
 // c3 (depth 2) -1.2 to -1.9%, c2 (depth 1) +0.7 to +1.1% (in-process A/B) — hence depth >= 2.
+// 1: primary rays of waves whose cone mask keeps no sphere normalise their direction only where they hit the board.
+#ifndef RT_LAZY_PRIMARY_U
+#define RT_LAZY_PRIMARY_U 1
+#endif
 #ifndef RT_SKIP_FAST_MIN_B
 #define RT_SKIP_FAST_MIN_B 2
 #endif
@@ -736,9 +740,13 @@ __device__ __forceinline__ void primary_sphere(const SceneView& V, const Ray& r,
 // cull makes the whole g_scene a miss, whatever the children say, so it can be tested after them.  `cone` (np >= kConeMin): bit k
 // set when sphere k < 64 may be hit by some ray of this wave (primary_cone_mask); the others are
 // provably missed and skipped.  Spheres are still visited in increasing k (tie order unchanged).
+// lazy_u (wave-uniform; trace): no sphere of the wave's cone mask is left (<= 64 spheres, all covered by the
+// mask) and the scene has no meshes, so only
+// the board can be hit and the direction u = unit(d) (the board test uses d) is computed here for the lanes that
+// hit it — the rest miss and never read it.
 template <bool FULL>
-__device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray& r, d3 bdP, double bdd,
-                                                   uint64_t cone, d3* hp) {
+__device__ __forceinline__ int closest_hit_primary(const SceneView& V, Ray& r, d3 bdP, double bdd,
+                                                   uint64_t cone, d3* hp, bool lazy_u = false) {
     const DevScene* S = V.S;
     int kind = -1;
     double best = -1.0;
@@ -790,6 +798,7 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, const Ray
         }
     }
     if (FULL) meshes_closest(V, r, eps, &kind, &best, hp);
+    if (lazy_u && kind >= 0) set_dir(&r, r.d, unit(r.d));
     // The bounding-sphere cull (:747-758) only turns hits into misses, so it is evaluated last and only
     // for rays that hit something: waves of background rays skip it.
     if (kind >= 0 && !bound_pass_dp(S, bdP, bdd, r.u)) kind = -1;
@@ -901,6 +910,9 @@ __device__ __forceinline__ float inf_if_nan(float v) { return v >= 0.0f ? v : __
 // and v = unit(C_k - o) is at most asin(R / |C_k - o|), i.e. |a - v| <= rho_d + chord(R / |C_k - o|).
 // FP32 coordinates carry < 2^-20 relative error; R gets 2^-12 (|o| + |C| + 1) absolute and the chord
 // test 2^-14 of slack.
+#ifndef RT_CHEAP_BUNDLE
+#define RT_CHEAP_BUNDLE 0
+#endif
 __device__ __forceinline__ uint64_t ray_bundle_part(const SceneView& V, bool on, const Ray& r, int f) {
     const int lane = __lane_id();
     const float ox = lane_f32(r.px, f), oy = lane_f32(r.py, f), oz = lane_f32(r.pz, f);
@@ -921,12 +933,29 @@ __device__ __forceinline__ uint64_t ray_bundle_part(const SceneView& V, bool on,
         const DevSphereF& c = V.sphf[lane];
         if (c.rm >= 0.0f) {                                   // padding spheres: rm = -inf
             const float vx = c.cx - ox, vy = c.cy - oy, vz = c.cz - oz;
-            const float D = msqrt(fmaf(vx, vx, fmaf(vy, vy, vz * vz)));
+            const float D2 = fmaf(vx, vx, fmaf(vy, vy, vz * vz));
+            const float D = msqrt(D2);
             const float Dm = D + rho_o;
             const float scale = fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz))) +
                                 fmaxf(fabsf(c.cx), fmaxf(fabsf(c.cy), fabsf(c.cz))) + 1.0f;
             const float R = (msqrt(fmaf(c.rm, 1.0f + 0x1p-20f, Dm * Dm * 0x1p-46f)) + rho_o) * (1.0f + 0x1p-12f) +
                             0x1p-12f * scale;
+#if RT_CHEAP_BUNDLE
+            // The same cone test without the chord's two square roots and the reciprocal of D: for s = R / D <= 0.9,
+            // chord(asin s) = s sqrt(2 / (1 + sqrt(1 - s^2))) <= s (1 + s^2 / 4) (equal at s = 0, 1.2% above the
+            // chord at s = 0.9; the gap only grows towards 0.9), so |a - v / D| <= rho_d + chord + 2^-14 follows from
+            // |a D - v| <= rho_d D + R (1 + s^2 / 4) + 2^-14 D (both sides times D > 0).  s > 0.9 (D < R / 0.9):
+            // kept, as D <= R is.  FP32 errors of a D - v (< 2^-21 D) and of s^2 (mrcp: 2^-22 relative) stay far
+            // inside the 2^-14 D slack.
+            if (!(D * 0.9f > R)) {
+                keep = true;
+            } else {
+                const float s2 = (R * R) * mrcp(D2);
+                const float limD = fmaf(rho_d + 0x1p-14f, D, R * fmaf(0.25f, s2, 1.0f));
+                const float ex = fmaf(ax, D, -vx), ey = fmaf(ay, D, -vy), ez = fmaf(az, D, -vz);
+                keep = !(fmaf(ex, ex, fmaf(ey, ey, ez * ez)) > limD * limD);
+            }
+#else
             if (!(D > R)) {
                 keep = true;
             } else {
@@ -935,6 +964,7 @@ __device__ __forceinline__ uint64_t ray_bundle_part(const SceneView& V, bool on,
                 const float ex = ax - vx * iD, ey = ay - vy * iD, ez = az - vz * iD;
                 keep = !(fmaf(ex, ex, fmaf(ey, ey, ez * ez)) > lim * lim);
             }
+#endif
         }
     }
     const uint64_t kept = __ballot(keep);
@@ -1289,7 +1319,7 @@ __device__ __forceinline__ void next_ray(d3 p, d3 nd, d3 nu, Ray* r) {
 template <int B, bool TRANSP, int SS = kSlotStride>
 __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool first, bool alive, d3 bdP, double bdd,
                                            uint64_t cone, Ray* r, int* levels,
-                                           double* slot, int* mslot, int* skip) {
+                                           double* slot, int* mslot, int* skip, bool lazy_u) {
     uint64_t smask = ~0ull;
     RT_COUNT(V.S, kCntLevels, 1);
     if (!first) {
@@ -1299,7 +1329,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     d3 p = mk(0.0, 0.0, 0.0);
     int kind = -1;
     if (alive) {
-        kind = first ? closest_hit_primary<TRANSP>(V, *r, bdP, bdd, cone, &p)
+        kind = first ? closest_hit_primary<TRANSP>(V, *r, bdP, bdd, cone, &p, lazy_u)
                      : closest_hit<TRANSP, true>(V, *r, &p, smask, TRANSP ? -1 : *skip, lvl > 0);
     }
     const bool hit = kind >= 0;
@@ -1357,7 +1387,13 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
     Ray r;
     r.p0 = p0;
     d3 d = sub(p1, p0);
-    set_dir(&r, d, unit(d));
+    // A primary ray of a wave whose cone mask keeps no sphere can only hit the board: its direction is computed
+    // by closest_hit_primary for the lanes that hit (sky waves skip the normalisation).
+    // (spheres past the first 64 are not in the mask: scenes with more always normalise)
+    const bool lazy_u = RT_LAZY_PRIMARY_U && PRIMARY && !TRANSP && V.np >= kPrimaryConeMin && V.np <= 64 &&
+                        (cone & sphere_bits(V.np)) == 0;
+    if (lazy_u) r.d = d;
+    else set_dir(&r, d, unit(d));
     // rays traced (seg, shadow) follow from `levels`: every lane traces levels 0 .. min(levels, B), nl shadow rays per hit
     int skip = -1;                                          // origin_skip of r's origin
     constexpr bool kSkip = !TRANSP && B >= RT_SKIP_FAST_MIN_B;  // fast loop: origin skips from this depth
@@ -1373,14 +1409,14 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
         const bool first = PRIMARY && lvl == 0;
         if (CULL) {
             if (!cull_level<B, TRANSP, SS>(V, lvl, first, alive, bdP, bdd, cone, &r, &levels, slot, mslot,
-                                           &skip))
+                                           &skip, lazy_u))
                 break;
         } else {
             d3 p = mk(0.0, 0.0, 0.0);
             int kind = -1;
             if (alive) {
                 if (first) {
-                    kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p);
+                    kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p, lazy_u);
                 } else {
                     set_origin_f32(S, &r);
                     kind = closest_hit<TRANSP>(V, r, &p, ~0ull, TRANSP ? -1 : skip, lvl > 0);

@@ -42,9 +42,11 @@ def main():
     moving = os.environ.get("MOVING", "0") == "1"      # a new eye every render (16-view orbit, as bench.py's leg)
     tmp = tempfile.mkdtemp()
     libs = {"base": load(abi.LIB_PATH, tmp, "base")}
+    only = set(os.environ["VARS"].split(",")) if os.environ.get("VARS") else None
     for d in sorted(glob.glob(os.path.join(ROOT, "tools", "_var", "*", "librt_amd.so"))):
         name = os.path.basename(os.path.dirname(d))
-        libs[name] = load(d, tmp, name)
+        if only is None or name in only:
+            libs[name] = load(d, tmp, name)
     st = torch.cuda.current_stream()
     ctxs, bufs = {}, {}
     for name, L in libs.items():
@@ -85,6 +87,23 @@ def main():
                 torch.cuda.synchronize()
                 if r:
                     res[(c, name)].append(e0.elapsed_time(e1) / reps)
+    # every build must produce the same images (byte for byte) as the in-tree one
+    for c in cfgs:
+        cfg = scenes.CONFIGS[c]
+        sa = cfg.scene().to_abi()
+        ref = None
+        for name, L in libs.items():
+            abi.check(L.rt_set_scene(ctxs[name], ctypes.byref(sa)), "rt_set_scene")
+            o32 = torch.empty((cfg.height, cfg.width, 4), dtype=torch.float32, device="cuda")
+            o8 = torch.empty((cfg.height, cfg.width, 4), dtype=torch.uint8, device="cuda")
+            abi.check(L.rt_render_dev(ctxs[name], ctypes.byref(cfg.camera()), cfg.width, cfg.height, cfg.depth, None,
+                                      ctypes.c_void_p(o32.data_ptr()), ctypes.c_void_p(o8.data_ptr()), None, None,
+                                      ctypes.c_void_p(st.cuda_stream)), "rt_render_dev")
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = (o32, o8)
+            elif not (torch.equal(o32, ref[0]) and torch.equal(o8, ref[1])):
+                print(json.dumps({"config": c, "lib": name, "error": "image differs from base"}), flush=True)
     for (c, name), v in res.items():
         base = statistics.median(res[(c, "base")])
         med = statistics.median(v)

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
-want() { case " ${STEPS:-tests guard copy c4 bench} " in *" $1 "*) return 0;; esac; return 1; }
+want() { case " ${STEPS:-tests guard copy c4 over diag bench} " in *" $1 "*) return 0;; esac; return 1; }
 if want tests; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} \
       > "$OUT/gpu_tests.log" 2>&1
@@ -26,6 +26,15 @@ if want c4; then
   timeout -k 10 300 python -u tools/c4_copy_probe.py > "$OUT/c4_copy.json" 2> "$OUT/c4_copy.err" \
       || { echo "c4 probe failed"; tail -20 "$OUT/c4_copy.err"; exit 12; }
   cat "$OUT/c4_copy.json"
+fi
+if want over; then
+  timeout -k 10 120 python -u tools/overhead_probe.py > "$OUT/overhead.json" 2> "$OUT/overhead.err" \
+      || { echo "overhead probe failed"; tail -20 "$OUT/overhead.err"; exit 13; }
+  cat "$OUT/overhead.json"
+fi
+if want diag; then
+  timeout -k 10 700 bash tools/gpu_diag.sh > "$OUT/diag.log" 2>&1
+  rc=$?; cat "$OUT/diag.log"; [ $rc -eq 0 ] || { echo "diag rc=$rc"; exit 14; }
 fi
 if want bench; then
   timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" \
