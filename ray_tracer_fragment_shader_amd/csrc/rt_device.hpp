@@ -304,6 +304,7 @@ struct SceneView {
     const DevMesh* mesh;             // global, wave-uniform reads
     const DevTri* tri;
     int np;                          // padded sphere count (wave-uniform)
+    int ns;                          // stride of the per-sphere arrays (a constant in the fast kernels)
     int nl;                          // light count (wave-uniform)
     int nm;                          // mesh count (wave-uniform)
     int hits_ok;                     // rays from this kernel's hit points may skip the bounding-sphere cull
@@ -318,21 +319,24 @@ __device__ __forceinline__ int hits_ok_from(const DevScene* S, d3 p0) {
     return (S->hits_inside != 0) & (dx * dx + dy * dy + dz * dz <= S->hits_lim2);
 }
 
-// hdr: header copy the kernel reads (LDS or global); g: the global record (for the filter images).
-__device__ __forceinline__ SceneView view_of(const DevScene* hdr, const DevScene* g, int np, int nl) {
+// hdr: header copy the kernel reads (LDS or global); g: the global record (for the filter images).  ns: the
+// arrays' stride (DevScene::n_stride; the fast kernels pass the constant kFastStride, so every record address is
+// the scene pointer plus a constant).
+__device__ __forceinline__ SceneView view_of(const DevScene* hdr, const DevScene* g, int np, int ns, int nl) {
     SceneView v;
     v.S = hdr;
     v.np = np;
+    v.ns = ns;
     v.nl = nl;
     v.sph = reinterpret_cast<const DevSphere*>(hdr + 1);
-    v.prim = reinterpret_cast<const DevSpherePrim*>(v.sph + np);
+    v.prim = reinterpret_cast<const DevSpherePrim*>(v.sph + ns);
     const DevSphere* gsph = reinterpret_cast<const DevSphere*>(g + 1);
-    const DevSpherePrim* gprim = reinterpret_cast<const DevSpherePrim*>(gsph + np);
-    v.sphf = reinterpret_cast<const DevSphereF*>(gprim + np);
-    v.primf = reinterpret_cast<const DevSpherePrimF*>(v.sphf + np);
-    v.cone = reinterpret_cast<const DevSphereCone*>(v.primf + np);
-    v.lightf = reinterpret_cast<const DevSphereLightF*>(v.cone + np);
-    v.mesh = reinterpret_cast<const DevMesh*>(v.lightf + (size_t)nl * np);
+    const DevSpherePrim* gprim = reinterpret_cast<const DevSpherePrim*>(gsph + ns);
+    v.sphf = reinterpret_cast<const DevSphereF*>(gprim + ns);
+    v.primf = reinterpret_cast<const DevSpherePrimF*>(v.sphf + ns);
+    v.cone = reinterpret_cast<const DevSphereCone*>(v.primf + ns);
+    v.lightf = reinterpret_cast<const DevSphereLightF*>(v.cone + ns);
+    v.mesh = reinterpret_cast<const DevMesh*>(v.lightf + (size_t)nl * ns);
     v.nm = g->n_meshes;
     v.tri = reinterpret_cast<const DevTri*>(v.mesh + v.nm);
     v.hits_ok = hdr->hits_ok;        // for the camera eye (rt_prepare_kernel); ray lists set it per ray
@@ -745,8 +749,8 @@ __device__ __forceinline__ void primary_sphere(const SceneView& V, const Ray& r,
 // the board can be hit and the direction u = unit(d) (the board test uses d) is computed here for the lanes that
 // hit it — the rest miss and never read it.
 template <bool FULL>
-__device__ __forceinline__ int closest_hit_primary(const SceneView& V, Ray& r, d3 bdP, double bdd,
-                                                   uint64_t cone, d3* hp, bool lazy_u = false) {
+__device__ __forceinline__ int closest_hit_primary(const SceneView& V, Ray& r, uint64_t cone, d3* hp,
+                                                   bool lazy_u = false) {
     const DevScene* S = V.S;
     int kind = -1;
     double best = -1.0;
@@ -801,7 +805,11 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, Ray& r, d
     if (lazy_u && kind >= 0) set_dir(&r, r.d, unit(r.d));
     // The bounding-sphere cull (:747-758) only turns hits into misses, so it is evaluated last and only
     // for rays that hit something: waves of background rays skip it.
-    if (kind >= 0 && !bound_pass_dp(S, bdP, bdd, r.u)) kind = -1;
+    // (deltaP = bc - eye, computed here for the waves that need it rather than held from the kernel's start)
+    if (kind >= 0) {
+        const d3 bdP = sub(ld3(S->bc), r.p0);               // :740 with p0 = camera
+        if (!bound_pass_dp(S, bdP, dot(bdP, bdP), r.u)) kind = -1;
+    }
     return kind;
 }
 
@@ -1017,7 +1025,7 @@ __device__ __forceinline__ uint64_t shadow_bundle_mask(const SceneView& V, bool 
     if (!(rho < 1.0f)) return ~0ull;
     bool keep = false;
     if (lane < V.np) {
-        const DevSphereLightF& c = V.lightf[li * V.np + lane];
+        const DevSphereLightF& c = V.lightf[li * V.ns + lane];
         if (c.c <= 1.0f) {
             const float lim = rho + msqrt(fmaxf(0.0f, 2.0f - 2.0f * c.c)) + 0x1p-14f;
             const float l2 = lim * lim;
@@ -1045,7 +1053,7 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
     const DevScene* S = V.S;
     if (!(RT_HITS_INSIDE && (RT_HITS_VIEW ? V.hits_ok : S->hits_ok)) && !bound_pass(S, r.p0, r.u)) return false;   // shadow rays start at hits
     const double eps = S->eps;
-    const DevSphereLightF* lf = V.lightf + li * V.np;
+    const DevSphereLightF* lf = V.lightf + li * V.ns;
     int k0 = 0;
     if (CULL && V.np >= kConeMin) {                               // mask: shadow_bundle_mask
         for (uint64_t m = mask & sphere_bits(V.np); m; m &= m - 1) {
@@ -1269,7 +1277,7 @@ __host__ __device__ constexpr int colour_slots(int B, bool transp) { return B + 
 // by that vector (:1238-1247),
 // so the colour is the right-nested local[0] + w[0] % (local[1] + w[1] % (...)).  TRANSP = false: all
 // materials opaque, no meshes, w = (1,1,1) (multiplication by 1.0 is exact) and any-hit shadows.
-// PRIMARY: p0 is the camera and V.prim/V.primf hold its per-sphere data; (bdP, bdd) = bc - eye, |.|^2;
+// PRIMARY: p0 is the camera and V.prim/V.primf hold its per-sphere data;
 // cone = primary_cone_mask of the wave (used when np >= kConeMin).
 // seg / shadow count the rays actually traced.
 // CULL (>= kConeMin spheres): called by all 64 lanes of a wave, the culling masks reduce over it.
@@ -1317,8 +1325,7 @@ __device__ __forceinline__ void next_ray(d3 p, d3 nd, d3 nu, Ray* r) {
 // One bounce level of the CULL variant, run by all lanes of the wave (ray_bundle_mask and shade's
 // shadow_bundle_mask reduce over it).  Returns false when no lane hit (the bounce loop ends).
 template <int B, bool TRANSP, int SS = kSlotStride>
-__device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool first, bool alive, d3 bdP, double bdd,
-                                           uint64_t cone, Ray* r, int* levels,
+__device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool first, bool alive, uint64_t cone, Ray* r, int* levels,
                                            double* slot, int* mslot, int* skip, bool lazy_u) {
     uint64_t smask = ~0ull;
     RT_COUNT(V.S, kCntLevels, 1);
@@ -1329,7 +1336,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     d3 p = mk(0.0, 0.0, 0.0);
     int kind = -1;
     if (alive) {
-        kind = first ? closest_hit_primary<TRANSP>(V, *r, bdP, bdd, cone, &p, lazy_u)
+        kind = first ? closest_hit_primary<TRANSP>(V, *r, cone, &p, lazy_u)
                      : closest_hit<TRANSP, true>(V, *r, &p, smask, TRANSP ? -1 : *skip, lvl > 0);
     }
     const bool hit = kind >= 0;
@@ -1380,7 +1387,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
 }
 
 template <int B, bool PRIMARY, bool TRANSP, bool CULL, int SS = kSlotStride>
-__device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, double bdd, uint64_t cone,
+__device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t cone,
                                     uint32_t* seg, uint32_t* shadow, double* slot, int* mslot) {
     const DevScene* S = V.S;
     int levels = 0;
@@ -1408,7 +1415,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
         if (!__any(alive)) break;                           // the whole wave has missed: early out
         const bool first = PRIMARY && lvl == 0;
         if (CULL) {
-            if (!cull_level<B, TRANSP, SS>(V, lvl, first, alive, bdP, bdd, cone, &r, &levels, slot, mslot,
+            if (!cull_level<B, TRANSP, SS>(V, lvl, first, alive, cone, &r, &levels, slot, mslot,
                                            &skip, lazy_u))
                 break;
         } else {
@@ -1416,7 +1423,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, d3 bdP, do
             int kind = -1;
             if (alive) {
                 if (first) {
-                    kind = closest_hit_primary<TRANSP>(V, r, bdP, bdd, cone, &p, lazy_u);
+                    kind = closest_hit_primary<TRANSP>(V, r, cone, &p, lazy_u);
                 } else {
                     set_origin_f32(S, &r);
                     kind = closest_hit<TRANSP>(V, r, &p, ~0ull, TRANSP ? -1 : skip, lvl > 0);

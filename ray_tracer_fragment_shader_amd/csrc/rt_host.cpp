@@ -326,13 +326,15 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
 
     const size_t bytes = (size_t)rt::scene_bytes_for(s->n_spheres, s->n_meshes, n_tris, s->n_lights);
     const int np = rt::padded_spheres(s->n_spheres);
+    const int ns = rt::sphere_stride(np);            // array stride (rt_layout.hpp)
     blob->assign(bytes, 0);
     rt::DevScene* d = reinterpret_cast<rt::DevScene*>(blob->data());
     rt::DevSphere* sph = reinterpret_cast<rt::DevSphere*>(d + 1);
-    rt::DevSpherePrim* prim = reinterpret_cast<rt::DevSpherePrim*>(sph + np);
-    rt::DevSphereF* sphf = reinterpret_cast<rt::DevSphereF*>(prim + np);
+    rt::DevSpherePrim* prim = reinterpret_cast<rt::DevSpherePrim*>(sph + ns);
+    rt::DevSphereF* sphf = reinterpret_cast<rt::DevSphereF*>(prim + ns);
     (void)prim;                                      // per-eye data: filled on the device (rt_prepare_kernel)
     d->n_padded = np;
+    d->n_stride = ns;
     d->lds_bytes = rt::lds_bytes_for(s->n_spheres);
     const double inf = std::numeric_limits<double>::infinity();
     d->eye[0] = d->eye[1] = d->eye[2] = std::numeric_limits<double>::quiet_NaN();
@@ -438,7 +440,7 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
         if ((double)rmf < rm) rmf = std::nextafter(rmf, std::numeric_limits<float>::infinity());
         sphf[k].rm = rmf;
     }
-    for (int k = s->n_spheres; k < np; ++k) {                                   // padding: never a hit
+    for (int k = s->n_spheres; k < ns; ++k) {                                   // padding: never a hit
         sph[k].r2 = -inf;
         sphf[k].rm = -std::numeric_limits<float>::infinity();
     }
@@ -448,12 +450,12 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     // inside or near a sphere (|C - L| <= r (1 + 2^-20) or |C - L| <= 2^-14 (1 + |L| + |C|)) gets c = -inf
     // (always tested), padding spheres c = +inf (never).
     rt::DevSphereLightF* lightf = reinterpret_cast<rt::DevSphereLightF*>(
-        reinterpret_cast<rt::DevSphereCone*>(reinterpret_cast<rt::DevSpherePrimF*>(sphf + np) + np) + np);
+        reinterpret_cast<rt::DevSphereCone*>(reinterpret_cast<rt::DevSpherePrimF*>(sphf + ns) + ns) + ns);
     for (int i = 0; i < s->n_lights; ++i) {
         const HP L = hp(s->lights[i].position);
         const double aL = std::max(std::fabs(L.x), std::max(std::fabs(L.y), std::fabs(L.z)));
-        for (int k = 0; k < np; ++k) {
-            rt::DevSphereLightF& f = lightf[i * np + k];
+        for (int k = 0; k < ns; ++k) {
+            rt::DevSphereLightF& f = lightf[i * ns + k];
             f.vx = f.vy = f.vz = 0.0f;
             if (k >= s->n_spheres) {
                 f.c = std::numeric_limits<float>::infinity();
@@ -480,7 +482,7 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     // Meshes (Tetrahedron :863-900, Cube :903-950): Shape(p, m, sqrt(3)*edge/2, false) with Triangle /
     // Quad sub-objects at zero position.  World vertex 0 of a triangle: tetrahedron (zero + (p + bc)) + v0,
     // cube (zero + (zero + (p + bc))) + v0 — the chain of `_position + positionOffset` additions (:739, :640).
-    rt::DevMesh* dmesh = reinterpret_cast<rt::DevMesh*>(lightf + (size_t)s->n_lights * np);
+    rt::DevMesh* dmesh = reinterpret_cast<rt::DevMesh*>(lightf + (size_t)s->n_lights * ns);
     rt::DevTri* dtri = reinterpret_cast<rt::DevTri*>(dmesh + s->n_meshes);
     d->n_meshes = s->n_meshes;
     d->n_tris = n_tris;

@@ -91,12 +91,12 @@ __global__ __launch_bounds__(256) void rt_cone_permute_kernel(const uint64_t* __
 // r2 = -inf, hence c0 = -inf: always rejected.
 __global__ __launch_bounds__(kThreads) void rt_prepare_kernel(DevScene* __restrict__ g, double ex, double ey,
                                                               double ez) {
-    const int np = g->n_padded;
+    const int np = g->n_padded, ns = g->n_stride;
     DevSphere* sph = reinterpret_cast<DevSphere*>(g + 1);
-    DevSpherePrim* prim = reinterpret_cast<DevSpherePrim*>(sph + np);
-    DevSphereF* sphf = reinterpret_cast<DevSphereF*>(prim + np);
-    DevSpherePrimF* primf = reinterpret_cast<DevSpherePrimF*>(sphf + np);
-    DevSphereCone* cone = reinterpret_cast<DevSphereCone*>(primf + np);
+    DevSpherePrim* prim = reinterpret_cast<DevSpherePrim*>(sph + ns);
+    DevSphereF* sphf = reinterpret_cast<DevSphereF*>(prim + ns);
+    DevSpherePrimF* primf = reinterpret_cast<DevSpherePrimF*>(sphf + ns);
+    DevSphereCone* cone = reinterpret_cast<DevSphereCone*>(primf + ns);
     const d3 eye = mk(ex, ey, ez);
     const int k = blockIdx.x * kThreads + threadIdx.x;
     if (k == 0) {
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(kThreads) void rt_scene_init_kernel(DevScene* __res
     const int k = blockIdx.x * kThreads + threadIdx.x;
     if (k == 0) g->rsquare = rcp_core(g->square);
     if (k < 2) g->tri[k].rden = g->tri[k].fast ? rcp_core(g->tri[k].den) : 0.0;
-    const SceneView V = view_of(g, g, g->n_padded, g->n_lights);
+    const SceneView V = view_of(g, g, g->n_padded, g->n_stride, g->n_lights);
     if (k < g->n_tris) {
         DevTri* t = const_cast<DevTri*>(V.tri) + k;
         t->rden = t->fast ? rcp_core(t->den) : 0.0;
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kThreads) void rt_intersect_kernel(const DevScene* 
                                                                 rt_hit* __restrict__ hits) {
     const int k = blockIdx.x * kThreads + threadIdx.x;
     if (k >= n) return;
-    const SceneView V = view_of(S, S, S->n_padded, S->n_lights);
+    const SceneView V = view_of(S, S, S->n_padded, S->n_stride, S->n_lights);
     Ray r;
     r.p0 = ld3(starts + 3 * k);
     d3 d = sub(ld3(ends + 3 * k), r.p0);
@@ -355,6 +355,7 @@ struct rt_ctx {
     int scene_bytes = 0;
     int lds_bytes = 0;
     int n_padded = 0;
+    int n_stride = 0;
     int n_lights = 0;
     bool scene_set = false;
     bool transparent = false;                  // some material is transparent: TRANSP kernel variants
@@ -579,6 +580,7 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     RT_HIP(hipDeviceSynchronize());
     c->lds_bytes = h->lds_bytes;
     c->n_padded = h->n_padded;
+    c->n_stride = h->n_stride;
     c->n_lights = h->n_lights;
     c->transparent = h->transparent != 0 || h->n_meshes > 0;   // FULL kernel variants
     c->tree = h->tree != 0;
@@ -626,6 +628,7 @@ static int render_params(const rt_ctx* c, const rt_camera* cam, int W, int H, in
     P->frame_rows = nl / P->frames;
     P->lds_bytes = c->lds_bytes;
     P->np = c->n_padded;
+    P->ns = c->n_stride;
     P->nl = c->n_lights;
     P->wg_staging = c->wg_staging;
 #if RT_WAVE_TRACE

@@ -2,16 +2,19 @@
 //
 // Layout in HBM (one allocation per rt_ctx):
 //   DevScene header
-//   DevSphere[np]       FP64 exact data                 ┐ copied into LDS once per workgroup
-//   DevSpherePrim[np]   primary-ray FP64 data (per eye)  ┘ (lds_bytes)
-//   DevSphereF[np]      FP32 filter image               ┐ read through the scalar cache (SGPR operands),
-//   DevSpherePrimF[np]  primary-ray FP32 filter (per eye)│ one batch of kChunk records per s_load group
-//   DevSphereCone[np]   primary-ray cone of each sphere (per eye): per-wave culling
-//   DevSphereLightF[nl][np]  shadow-ray FP32 cone filter ┘ per light (line through the light)
+//   DevSphere[ns]       FP64 exact data                 ┐ copied into LDS once per workgroup
+//   DevSpherePrim[ns]   primary-ray FP64 data (per eye)  ┘ (lds_bytes)
+//   DevSphereF[ns]      FP32 filter image               ┐ read through the scalar cache (SGPR operands),
+//   DevSpherePrimF[ns]  primary-ray FP32 filter (per eye)│ one batch of kChunk records per s_load group
+//   DevSphereCone[ns]   primary-ray cone of each sphere (per eye): per-wave culling
+//   DevSphereLightF[nl][ns]  shadow-ray FP32 cone filter ┘ per light (line through the light)
 //   DevMesh[nm]         tetrahedra / cubes: bounding sphere, triangle range, material, child index
 //   DevTri[nt]          their triangles (world vertex 0, u, v, n, uv, uu, vv, den)
 // np = n_spheres rounded up to kChunk; the padding spheres have r2 = -inf and filter terms = -inf, so
-// they are rejected by the filter and can never hit.  The two *Prim arrays and DevSphereCone depend on
+// they are rejected by the filter and can never hit.  ns = the arrays' stride: np, except for scenes the fast
+// (non-culling) kernels render (np < kConeMin), whose arrays all have the fixed stride kFastStride — those kernels
+// then address every record at a constant offset from the scene pointer instead of holding six array pointers
+// in SGPRs (the SGPR budget of a seventh wave per SIMD).  The two *Prim arrays and DevSphereCone depend on
 // the camera eye and are (re)written on the device by rt_prepare_kernel whenever rt_render_dev sees a
 // new eye.
 #pragma once
@@ -25,6 +28,8 @@ constexpr int kChunk = 4;              // spheres per branch-free filter batch
 #define RT_CONE_MIN 16
 #endif
 constexpr int kConeMin = RT_CONE_MIN;   // per-wave culling (primary cones, ray and shadow bundles) from this many (padded) spheres
+constexpr int kFastStride = kConeMin - kChunk;   // the array stride of every scene with np < kConeMin
+inline constexpr int sphere_stride(int np) { return np < kConeMin ? kFastStride : np; }
 // The primary-ray cone mask is one ballot per wave (fast FP32 math): from 8 spheres it beats the per-sphere
 // FP32 filter batches it replaces (same-box A/B: c2 -0.8%, c3 -1.9%; from 4 spheres c1 +3.7%).
 #ifndef RT_PRIMARY_CONE_MIN
@@ -123,6 +128,7 @@ struct alignas(16) DevScene {
     int32_t has_board;
     int32_t n_spheres;                 // real spheres
     int32_t n_padded;                  // np: n_spheres rounded up to kChunk
+    int32_t n_stride;                  // ns: stride of the per-sphere arrays (sphere_stride(np))
     int32_t n_lights;
     int32_t lds_bytes;                 // header + DevSphere[np] + DevSpherePrim[np]
     int32_t n_meshes;
@@ -140,14 +146,15 @@ struct alignas(16) DevScene {
 inline constexpr int padded_spheres(int n) { return (n + kChunk - 1) / kChunk * kChunk; }
 
 inline constexpr int lds_bytes_for(int n) {
-    return (int)(sizeof(DevScene) + (sizeof(DevSphere) + sizeof(DevSpherePrim)) * (unsigned)padded_spheres(n));
+    return (int)(sizeof(DevScene) +
+                 (sizeof(DevSphere) + sizeof(DevSpherePrim)) * (unsigned)sphere_stride(padded_spheres(n)));
 }
 
 inline constexpr int scene_bytes_for(int n, int n_meshes = 0, int n_tris = 0, int n_lights = 0) {
     return lds_bytes_for(n) +
            (int)((sizeof(DevSphereF) + sizeof(DevSpherePrimF) + sizeof(DevSphereCone) +
                   sizeof(DevSphereLightF) * (unsigned)n_lights) *
-                 (unsigned)padded_spheres(n)) +
+                 (unsigned)sphere_stride(padded_spheres(n))) +
            (int)(sizeof(DevMesh) * (unsigned)n_meshes + sizeof(DevTri) * (unsigned)n_tris);
 }
 

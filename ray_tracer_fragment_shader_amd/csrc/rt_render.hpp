@@ -22,6 +22,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 
 #include "../../include/rt_api.h"
 #include "rt_device.hpp"
@@ -50,10 +51,10 @@
 #define RT_MINW_CULL 5                         // the culling variant (>= kConeMin spheres): 87 VGPRs, no spills
 #endif
 // Default launch-bound waves per SIMD of the fast kernels by depth: 6 up to depth 2, 5 from depth 3.  The bound
-// is a floor: the depth 1 kernel comes out at 71 VGPRs under it (7 waves by VGPRs; the c2 kernel accumulates
-// its colour in LDS, shade ACC), but its 106 SGPRs hold it at 6 waves per SIMD on the hardware (see
-// rt_render_kernel_sg); a bound of 7 made the compiler trade SGPR spills (v_writelane) for the same VGPRs and ran
-// c2 +2.3% slower (same-box A/B).
+// is a floor: the depth 1 and 2 kernels come out at 63 / 67 VGPRs under it (8 / 7 waves by VGPRs; the c2 kernel
+// accumulates its colour in LDS, shade ACC) and their SGPR cap (rt_render_kernel_sg, 96) gives them 7 waves per
+// SIMD on the hardware; r03's bound of 7 made the compiler trade SGPR spills (v_writelane) for the same VGPRs and
+// ran c2 +2.3% slower (same-box A/B).
 __host__ __device__ constexpr int kDefaultMinWaves(int B) { return B <= 2 ? 6 : 5; }
 // RT_MAX_B < 7 (experiment builds only, tools/variants.sh): deeper kernels are not instantiated.
 #ifndef RT_MAX_B
@@ -114,7 +115,44 @@ struct RenderParams {
     uint64_t* wtrace;                          // RT_WAVE_TRACE builds: per-wave {start, end, HW_ID}
     const uint64_t* cone_in;                   // this view's primary cone masks in dispatch order (or nullptr)
     uint64_t* cone_out;                        // calibration render: each tile's mask, by tile (or nullptr)
+    int32_t ns;                                // stride of the scene's per-sphere arrays (DevScene::n_stride)
 };
+
+// The render kernels' arguments, in order: the kernel-argument segment lays them out as this struct (each at its
+// natural alignment), which late_outputs() relies on.  (The kernels take them as separate parameters: one
+// by-value struct parameter measured +11 VGPRs in the culling kernel.)
+struct RenderArgs {
+    const DevScene* scene;
+    RenderParams P;
+    void* o32;                                 // float image (RGBA32F / GRAY32F) or nullptr
+    void* o8;                                  // byte image (RGBA8 / RGB8 / GRAY8) or nullptr
+    double* o64;                               // RGB64F parity image or nullptr
+    uint32_t* orc;                             // per-pixel ray counters or nullptr
+    const int32_t* tile_rows;                  // dispatch order of tile rows (nullptr: bottom to top)
+    const uint64_t* cone_in;                   // cached primary cone masks (nullptr: computed in the kernel)
+};
+
+// The output pointers, read from the kernel-argument segment where the stores need them: scalar loads behind an
+// opaque copy of the segment pointer, so the compiler cannot hoist them to the kernel's start and hold 8 SGPRs
+// through the whole trace (the SGPR budget of a seventh wave per SIMD).
+struct RenderOuts {
+    void* o32;
+    void* o8;
+    double* o64;
+    uint32_t* orc;
+};
+__device__ __forceinline__ RenderOuts late_outputs() {
+    typedef const __attribute__((address_space(4))) char* kptr;
+    typedef void* const __attribute__((address_space(4)))* kpp;
+    kptr ka = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    RenderOuts o;
+    o.o32 = *(kpp)(ka + offsetof(RenderArgs, o32));
+    o.o8 = *(kpp)(ka + offsetof(RenderArgs, o8));
+    o.o64 = (double*)*(kpp)(ka + offsetof(RenderArgs, o64));
+    o.orc = (uint32_t*)*(kpp)(ka + offsetof(RenderArgs, orc));
+    return o;
+}
 
 // Image row (within its frame) of local row lr; local rows are frame-major (rt_rows.frames).
 __device__ __forceinline__ int global_row_of(const RenderParams& P, int lr) {
@@ -182,8 +220,6 @@ __device__ __forceinline__ void store_pixel(const RenderParams& P, size_t k, d3 
 template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false,
           bool PACKED = false>
 __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene, RenderParams P,
-                                            void* __restrict__ out32, void* __restrict__ out8,
-                                            double* __restrict__ out64, uint32_t* __restrict__ outrc,
                                             const int32_t* __restrict__ tile_rows,
                                             const uint64_t* __restrict__ cone_in) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -211,7 +247,9 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     uint32_t* strc = reinterpret_cast<uint32_t*>(smem + off + 4096 + 6144);             // [8][32] 1 KB
     uchar4* st8 = reinterpret_cast<uchar4*>(smem + off + 4096 + 6144 + 1024);           // [8][32] 1 KB
     if (LDS) __syncthreads();
-    const SceneView V = view_of(S, gscene, P.np, P.nl);
+    // the fast kernels (scenes with np < kConeMin) see the fixed array stride as a constant
+    constexpr bool kFixed = !LDS && !TRANSP && !CULL && !TREE && WG == RT_WG_FAST && RT_WG_FAST != kThreads;
+    const SceneView V = view_of(S, gscene, P.np, kFixed ? kFastStride : P.ns, P.nl);
     const d3 eye = ld3(P.eye);
 
     const int wave = tid >> 6, lane = tid & 63;
@@ -240,6 +278,9 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     asm volatile("" ::"s"(cone_cached), "s"(ty_raw));
     const bool pad = (unsigned)ty_raw >= (unsigned)P.tile_rows_n;
     const int ty = pad ? P.tile_rows_n - 1 : ty_raw;
+    // the stores' tile row: past every local row for padding positions (their bounds check fails), so no flag
+    // needs to live through the trace
+    const int ty_st = pad ? (1 << 27) : ty_raw;
     const int i = tx * TW + cx;
     const int lr = ty * kTileH + cy;
     const bool valid = i < P.width && lr < P.local_rows && !pad;
@@ -283,7 +324,6 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     // Primary ray Line(camera, sp), SURVEY.md Appendix B (basis: rayTraceScreen :1270-1279).
     const d3 sp = add(add(ld3(P.look), scl(P.pitch * (double)(ic + P.bottom_x), right)),
                       scl(P.pitch * (double)(j + P.bottom_y), upp));
-    const d3 bdP = sub(ld3(V.S->bc), eye);                  // bounding-sphere deltaP for p0 = camera
 #if RT_WAVE_TRACE
     const uint64_t t_mid = __builtin_amdgcn_s_memrealtime();   // prologue done: the primary ray is formed
 #endif
@@ -291,7 +331,7 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     if constexpr (TREE)
         col = trace_tree<B>(V, eye, sp, &seg, &sh);
     else
-        col = trace<B, true, TRANSP, CULL, WG>(V, eye, sp, bdP, dot(bdP, bdP), cone, &seg, &sh, slot, mslot);
+        col = trace<B, true, TRANSP, CULL, WG>(V, eye, sp, cone, &seg, &sh, slot, mslot);
 
     if (WG != kThreads || !P.wg_staging) {
         // Direct stores: each wave writes its 8 x 8 block as 8 row segments (128 B of RGBA32F each) and
@@ -301,15 +341,16 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
         asm volatile("" : "+v"(tid_e));
 #endif
         const int lane_e = tid_e & 63;
-        const int i_e = tx * TW + (tid_e >> 6) * bw + (lane_e & 7), lr_e = ty * kTileH + (lane_e >> 3);
-        if (i_e < P.width && lr_e < P.local_rows && !pad) {
+        const int i_e = tx * TW + (tid_e >> 6) * bw + (lane_e & 7), lr_e = ty_st * kTileH + (lane_e >> 3);
+        if (i_e < P.width && lr_e < P.local_rows) {
+            const RenderOuts O = late_outputs();
             const size_t k = (size_t)lr_e * P.width + i_e;
-            store_pixel<PACKED>(P, k, col, out32, out8);
-            if (out64) { out64[3 * k] = col.x; out64[3 * k + 1] = col.y; out64[3 * k + 2] = col.z; }
-            if (outrc) outrc[k] = seg | (sh << 16);
+            store_pixel<PACKED>(P, k, col, O.o32, O.o8);
+            if (O.o64) { O.o64[3 * k] = col.x; O.o64[3 * k + 1] = col.y; O.o64[3 * k + 2] = col.z; }
+            if (O.orc) O.orc[k] = seg | (sh << 16);
         }
-        if (P.row_cost && tid == 0 && !pad)
-            atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
+        if (P.row_cost && tid == 0 && ty_st < P.tile_rows_n)
+            atomicAdd(P.row_cost + ty_st, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
 #if RT_WAVE_TRACE
         if (P.wtrace && tid == 0) {
             const size_t w = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
@@ -328,6 +369,11 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     }
     // Stage through LDS, then store whole tile rows (RGBA formats only: the host routes packed formats to the
     // direct-store variants).
+    const RenderOuts O = late_outputs();
+    void* const out32 = O.o32;
+    void* const out8 = O.o8;
+    double* const out64 = O.o64;
+    uint32_t* const outrc = O.orc;
     const int ts = cy * kTileW + cx;
     if (out32) st32[ts] = make_float4((float)col.x, (float)col.y, (float)col.z, 1.0f);
     if (out64) { st64[3 * ts] = col.x; st64[3 * ts + 1] = col.y; st64[3 * ts + 2] = col.z; }
@@ -336,7 +382,7 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     __syncthreads();
     const int oy = tid >> 5, ox = tid & 31;
     const int gi = tx * kTileW + ox, glr = ty * kTileH + oy;
-    if (gi < P.width && glr < P.local_rows && !pad) {
+    if (gi < P.width && glr < P.local_rows && !pad) {                     // (A/B variant: pad kept)
         const size_t k = (size_t)glr * P.width + gi;
         if (out32) reinterpret_cast<float4*>(out32)[k] = st32[tid];
         if (out64) {
@@ -350,35 +396,33 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     if (P.row_cost && tid == 0 && !pad) atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
 }
 
+// (out32 .. outrc are read by late_outputs() from the argument segment, not through the parameters)
 template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false,
           bool PACKED = false>
-__global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene,
-                                                             RenderParams P, void* __restrict__ out32,
-                                                             void* __restrict__ out8,
-                                                             double* __restrict__ out64,
-                                                             uint32_t* __restrict__ outrc,
+__global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene, RenderParams P,
+                                                             void* out32, void* out8, double* out64, uint32_t* outrc,
                                                              const int32_t* __restrict__ tile_rows,
                                                              const uint64_t* __restrict__ cone_in) {
-    render_body<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED>(gscene, P, out32, out8, out64, outrc, tile_rows,
-                                                              cone_in);
+    render_body<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED>(gscene, P, tile_rows, cone_in);
 }
 
 // The same kernel with its SGPRs capped at RT_FAST_SGPRS (amdgpu_num_sgpr: a constant, hence a kernel of its
-// own).  The hardware keeps a wave's SGPRs in granules of 16 and fits 7 one-wave workgroups per SIMD only up to
-// 96 SGPRs per wave (tools/mb_slots.cpp: 71 VGPRs with 96 SGPRs -> 7 waves, with 98 -> 6) — the compiler's
-// occupancy estimate (7 at 106) assumes a larger SGPR file.  RT_FAST_SGPRS=96 runs the depth <= RT_SG_MAX_B fast
-// kernels with the cap: c2 then holds 7 waves per SIMD (wave trace: 7,168 resident) with 19 SGPRs spilled to
-// VGPR lanes, and measured +1.1% (same-box A/B) — the seventh wave does not pay for the spills, so off.
+// own).  The hardware fits 7 one-wave workgroups per SIMD only up to 96 SGPRs per wave (the compiler's
+// TotalSGPRs, VCC and friends included) and 8 only up to 78 (tools/mb_slots.cpp: 71 VGPRs with 96 SGPRs -> 7
+// waves, 98 -> 6; 63 VGPRs with 78 -> 8, 86 -> 7) — the compiler's occupancy estimate assumes a larger SGPR file.
+// r03: the cap cost 19 SGPR spills (+1.1%), so it was off.  r04: with the output pointers read at the stores
+// (late_outputs), the fixed array stride of the fast kernels and the bounding-sphere delta formed where it is
+// tested, the uncapped c2 kernel needs 98 SGPRs / 62 VGPRs and the capped one 94 / 63 with 2 spills: 7 waves per
+// SIMD, c2 -1.7% and c3 -2.5% against the uncapped build (same-box in-process A/B, tools/ab_libs.py); a cap of 80
+// (8 waves, 14 spills) ran +0.8%.
 #ifndef RT_FAST_SGPRS
-#define RT_FAST_SGPRS 0
+#define RT_FAST_SGPRS 96
 #endif
 template <int B, int MINW, bool CULL, bool PACKED>
 __global__ __launch_bounds__(RT_WG_FAST, MINW) __attribute__((amdgpu_num_sgpr(RT_FAST_SGPRS)))
-void rt_render_kernel_sg(const DevScene* __restrict__ gscene, RenderParams P, void* __restrict__ out32,
-                         void* __restrict__ out8, double* __restrict__ out64, uint32_t* __restrict__ outrc,
-                         const int32_t* __restrict__ tile_rows, const uint64_t* __restrict__ cone_in) {
-    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED>(gscene, P, out32, out8, out64, outrc, tile_rows,
-                                                                    cone_in);
+void rt_render_kernel_sg(const DevScene* __restrict__ gscene, RenderParams P, void* out32, void* out8, double* out64,
+                         uint32_t* outrc, const int32_t* __restrict__ tile_rows, const uint64_t* __restrict__ cone_in) {
+    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED>(gscene, P, tile_rows, cone_in);
 }
 
 // rayTraceRay on a list of rays Line(starts[k], ends[k]).  Rays from arbitrary starts: whether their hit
@@ -393,7 +437,7 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
     // Every lane traces (trace() reduces over the wave); lanes past n repeat ray n - 1 and store nothing.
     const int k = blockIdx.x * kThreads + threadIdx.x, kk = k < n ? k : n - 1;
     uint32_t seg = 0, sh = 0;
-    SceneView V = view_of(S, S, S->n_padded, S->n_lights);
+    SceneView V = view_of(S, S, S->n_padded, S->n_stride, S->n_lights);
     const d3 p0 = ld3(starts + 3 * kk);
     V.hits_ok = hits_ok_from(S, p0);
     double* slot = reinterpret_cast<double*>(smem) + threadIdx.x;
@@ -402,8 +446,7 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
     if constexpr (TREE)
         c = trace_tree<B>(V, p0, ld3(ends + 3 * kk), &seg, &sh);
     else
-        c = trace<B, false, TRANSP, false>(V, p0, ld3(ends + 3 * kk), mk(0.0, 0.0, 0.0), 0.0, ~0ull, &seg, &sh, slot,
-                                           mslot);
+        c = trace<B, false, TRANSP, false>(V, p0, ld3(ends + 3 * kk), ~0ull, &seg, &sh, slot, mslot);
     if (k >= n) return;
     if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
     if (rc) rc[k] = seg | (sh << 16);
@@ -475,14 +518,15 @@ hipError_t launch_render_one(const RenderLaunch& L) {
     return hipGetLastError();
 }
 
-// The SGPR-capped fast kernel (rt_render_kernel_sg) for the depths whose fast kernels fit 7 waves by VGPRs.
+// The SGPR-capped fast kernel (rt_render_kernel_sg) for the depths whose fast kernels fit 7 waves by VGPRs (c2: 63,
+// c3: 67).
 #ifndef RT_SG_MAX_B
-#define RT_SG_MAX_B 1
+#define RT_SG_MAX_B 2
 #endif
 template <int B, int MINW, bool PACKED>
 hipError_t launch_render_sg(const RenderLaunch& L) {
-    hipLaunchKernelGGL((rt_render_kernel_sg<B, MINW, false, PACKED>), L.grid, dim3(RT_WG_FAST), L.lds, L.stream, L.scene,
-                       L.P, L.o32, L.o8, L.o64, L.orc, L.P.tile_rows, L.P.cone_in);
+    hipLaunchKernelGGL((rt_render_kernel_sg<B, MINW, false, PACKED>), L.grid, dim3(RT_WG_FAST), L.lds, L.stream,
+                       L.scene, L.P, L.o32, L.o8, L.o64, L.orc, L.P.tile_rows, L.P.cone_in);
     return hipGetLastError();
 }
 

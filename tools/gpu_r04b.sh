@@ -1,0 +1,39 @@
+#!/bin/bash
+# Round-4 session B: GPU tests at HEAD, the wave-slot probe (SGPR thresholds at 63 VGPRs), the in-process A/B of
+# tools/_var builds (VARS) at c2/c3/c5, and the bench line.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=$(pwd)/gpurun_out
+mkdir -p "$OUT"
+want() { case " ${STEPS:-tests slots ab ctrace bench} " in *" $1 "*) return 0;; esac; return 1; }
+if want tests; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} \
+      > "$OUT/gpu_tests.log" 2>&1
+  rc=$?; tail -5 "$OUT/gpu_tests.log"; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit $rc; }
+fi
+if want slots && [ -x tools/_var/mb_slots ]; then
+  timeout -k 10 60 tools/_var/mb_slots > "$OUT/slots.jsonl" 2>&1 || { echo "slots failed"; cat "$OUT/slots.jsonl"; exit 5; }
+  cat "$OUT/slots.jsonl"
+fi
+if want ab; then
+  VARS=${VARS:-old,sg96,sg80} timeout -k 10 600 python -u tools/ab_libs.py ${CONFIGS:-c2,c3,c5} ${ROUNDS:-9} \
+      > "$OUT/ab.jsonl" 2> "$OUT/ab.err" || { echo "ab failed"; tail -20 "$OUT/ab.err"; exit 6; }
+  cat "$OUT/ab.jsonl"
+fi
+if want bench; then
+  timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" \
+      || { echo "bench failed"; tail -30 "$OUT/bench.err"; exit 3; }
+  python3 -c "import json; d=json.load(open('$OUT/bench.json')); print(d['value'], d['ms_per_step'], d['roofline']['kernel_ms_serial'], d['roofline']['interval_ms_in_flight'], {k: v.get('kernel_ms_serial') for k, v in d.get('configs', {}).items()}, d.get('drop_in', {}).get('moving_camera', {}).get('ms_per_frame'))"
+fi
+if want ctrace; then
+  cd /tmp && export TMPDIR=/tmp
+  for spec in "1 0 1" "0 16 2" "0 0 2"; do
+    set -- $spec
+    rm -rf "$OUT/ctrace_$1_$2_$3"
+    RT_COPY_MODE=$1 RT_COPY_BLOCKS=$2 DEPTH=$3 timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv \
+        -d "$OUT/ctrace_$1_$2_$3" -o run -- python3 "$GRAFT_REPO_ROOT/tools/copy_trace.py" > "$OUT/ctrace_$1_$2_$3.json" \
+        2> "$OUT/ctrace_$1_$2_$3.err" || { echo "ctrace $spec failed"; tail -5 "$OUT/ctrace_$1_$2_$3.err"; exit 7; }
+    cat "$OUT/ctrace_$1_$2_$3.json"; python3 "$GRAFT_REPO_ROOT/tools/copy_trace.py" parse "$OUT/ctrace_$1_$2_$3"
+  done
+  cd "$GRAFT_REPO_ROOT"
+fi

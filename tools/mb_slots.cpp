@@ -28,6 +28,14 @@ __global__ __launch_bounds__(64) void spin(uint64_t* rec, uint64_t ticks) {
     if constexpr (NV == 1094) asm volatile("" ::: "v70", "s93");
     if constexpr (NV == 1096) asm volatile("" ::: "v70", "s95");
     if constexpr (NV == 1098) asm volatile("" ::: "v70", "s97");
+    // 63 VGPRs (8 waves by VGPRs) and NV - 2000 SGPRs: where the SGPR budget costs the eighth / seventh wave (r04)
+    if constexpr (NV == 2064) asm volatile("" ::: "v62", "s63");
+    if constexpr (NV == 2072) asm volatile("" ::: "v62", "s71");
+    if constexpr (NV == 2080) asm volatile("" ::: "v62", "s79");
+    if constexpr (NV == 2084) asm volatile("" ::: "v62", "s83");
+    if constexpr (NV == 2088) asm volatile("" ::: "v62", "s87");
+    if constexpr (NV == 2092) asm volatile("" ::: "v62", "s91");
+    if constexpr (NV == 2096) asm volatile("" ::: "v62", "s95");
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
     if (threadIdx.x == 0) {
         lds[0] = 1;
@@ -82,6 +90,13 @@ int main() {
         run<1094>(d, h, n, lds);
         run<1096>(d, h, n, lds);
         run<1098>(d, h, n, lds);
+        run<2064>(d, h, n, lds);
+        run<2072>(d, h, n, lds);
+        run<2080>(d, h, n, lds);
+        run<2084>(d, h, n, lds);
+        run<2088>(d, h, n, lds);
+        run<2092>(d, h, n, lds);
+        run<2096>(d, h, n, lds);
     }
     hipFree(d);
     return 0;
