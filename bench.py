@@ -22,8 +22,9 @@ Extra legs in the same JSON line (outside the timed region of `value`):
   * "configs" (N = 1): c3 and c5 on one GPU (ms/frame, Mray/s, HBM-write and FP64 roofline fractions);
   * "drop_in" (N = 1): rt_render, the synchronous host-buffer call that replaces draw()'s rayTraceScreen,
     per call host to host at c2 (RGBA8 back to the host), and a moving camera (a new eye every frame);
-  * "roofline" / "roofline_fp64" of the dominant kernel and "cpu_baseline" (the bit-exact C restatement,
-    oracle/rt_oracle.c, best of 3 blocks of whole frames on this host's cores, rank 0 at N=1 only).
+  * "roofline" / "roofline_fp64" of the dominant kernel and "cpu_baseline" (the reference's own rayTraceRay built
+    from its sources, oracle/_ref, when the build travelled with the tree, else the bit-exact C restatement
+    oracle/rt_oracle.c; best of 3 blocks of whole frames on this host's CPU share, rank 0 at N=1 only).
 """
 from __future__ import annotations
 
@@ -308,13 +309,13 @@ def serial_kernel_ms(torch, L, abi, launch, stream, n=20):
 def packed_host_legs(t, sa, cam, W, H, B, k=30):
     """draw()'s host frame in the narrowest exact format (rt_render_packed, GRAY8 for the achromatic c2 scene:
     2.1 MB over PCIe instead of 8.3 MB), synchronous and pipelined (rt_render_packed_async + rt_ctx_wait: the copy of
-    frame k overlaps the render of frame k+1), into pinned memory from rt_host_alloc."""
+    frame k runs beside the render of frame k+1), into pinned memory from rt_host_alloc."""
     import ctypes
 
     from ray_tracer_fragment_shader_amd import abi
     L = abi.lib()
     pins = []
-    for _ in range(2):
+    for _ in range(3):
         p = ctypes.c_void_p()
         abi.check(L.rt_host_alloc(W * H, ctypes.byref(p)), "rt_host_alloc")
         pins.append(p)
@@ -328,20 +329,23 @@ def packed_host_legs(t, sa, cam, W, H, B, k=30):
         for _ in range(k):
             abi.check(L.rt_render_packed(*a, pins[0], None), "rt_render_packed")
         out["rt_render_packed_gray8_ms_per_call"] = round((time.perf_counter() - t0) / k * 1e3, 4)
-        tk = [ctypes.c_uint64(), ctypes.c_uint64()]
-        for f in range(4):
-            abi.check(L.rt_render_packed_async(*a, pins[f & 1], ctypes.byref(tk[f & 1])), "rt_render_packed_async")
-        abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
-        t0 = time.perf_counter()
-        for f in range(k):                                  # the draw() loop: queue frame f, show frame f-1
-            abi.check(L.rt_render_packed_async(*a, pins[f & 1], ctypes.byref(tk[f & 1])), "rt_render_packed_async")
-            if f:
-                abi.check(L.rt_ctx_wait(t._ctx, tk[(f - 1) & 1].value), "rt_ctx_wait")
-        abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
-        out["rt_render_packed_async_gray8_ms_per_frame"] = round((time.perf_counter() - t0) / k * 1e3, 4)
+        tk = [ctypes.c_uint64() for _ in range(3)]
+        for depth, key in ((1, "rt_render_packed_async_gray8_ms_per_frame"),
+                           (2, "rt_render_packed_async_gray8_ms_per_frame_2_behind")):
+            for f in range(4):
+                abi.check(L.rt_render_packed_async(*a, pins[f % 3], ctypes.byref(tk[f % 3])), "rt_render_packed_async")
+            abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
+            t0 = time.perf_counter()
+            for f in range(k):                              # the draw() loop: queue frame f, show frame f - depth
+                abi.check(L.rt_render_packed_async(*a, pins[f % 3], ctypes.byref(tk[f % 3])), "rt_render_packed_async")
+                if f >= depth:
+                    abi.check(L.rt_ctx_wait(t._ctx, tk[(f - depth) % 3].value), "rt_ctx_wait")
+            abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
+            out[key] = round((time.perf_counter() - t0) / k * 1e3, 4)
         out["packed_note"] = ("c2 frame as GRAY8 (2.07 MB: the scene is achromatic, rt_scene_achromatic) into pinned "
-                              "memory: synchronous per call, and pipelined (queue frame f, wait for frame f-1: one "
-                              "frame of latency, the copy of f overlaps the render of f+1)")
+                              "memory: synchronous per call (render + copy kernel on the render stream), and pipelined "
+                              "(queue frame f, wait for frame f-1 — one frame of latency — or f-2: the SDMA copy of a "
+                              "frame on the copy stream runs beside the next frame's render)")
     finally:
         for p in pins:
             L.rt_host_free(p)
@@ -373,6 +377,67 @@ def dropin_binding_legs(W, H, B, cfg, frames=30):
     res["note"] = (f"lib/rt_dropin --frames {frames} (the committed INTEGRATION.md binding, C++, built against "
                    "rt_api.h): its own steady-state ms per draw() after the first frame, host to host")
     return res
+
+
+def cpu_sample(render, seconds):
+    """Best of 3 blocks of whole frames, each about seconds / 3 of wall time -> (blocks [(frames, s)], best)."""
+    render()                                                 # warm (library load, page faults)
+    blocks = []
+    for _ in range(3):
+        n, t0 = 0, time.perf_counter()
+        while n < 1 or time.perf_counter() - t0 < seconds / 3:
+            render()
+            n += 1
+        blocks.append((n, time.perf_counter() - t0))
+    return blocks, max(blocks, key=lambda b: b[0] / b[1])
+
+
+def cpu_baseline(args, cfg, scene, cam, W, H, B, rays_frame):
+    """The CPU path timed on this host (rank 0, N = 1): the reference's own rayTraceRay compiled from its sources
+    (oracle/_ref/libref.so: built in the build container by oracle/Makefile, it travels with the tree; kind
+    "reference") when present, over the same rows with OpenMP on the host's CPU share, checked against the golden
+    frame hash; else the bit-exact C restatement (kind "port").  The port is timed beside it either way."""
+    from oracle import pyoracle as po
+    from tests import golden
+    nt = cpu_threads()
+    sa = scene.to_abi()
+    pblocks, pbest = cpu_sample(lambda: po.render(sa, cam, W, H, B, nthreads=nt),
+                                args.cpu_seconds / 2 if os.path.exists(po.REF_SO) else args.cpu_seconds)
+    port = rays_frame * pbest[0] / pbest[1] / 1e6
+    n1, t1 = 0, time.perf_counter()                          # one thread, for the per-core rate
+    while n1 < 1 or time.perf_counter() - t1 < 2.0:
+        po.render(sa, cam, W, H, B, nthreads=1)
+        n1 += 1
+    per_core = rays_frame * n1 / (time.perf_counter() - t1) / 1e6
+    common = {"unit": "Mray/s", "cores": nt, "threads_used": nt, "nproc": os.cpu_count(),
+              "affinity_cores": affinity_cores(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+              "host_cpu": cpu_model()}
+    port_desc = (f"oracle/rt_oracle.c (bit-exact restatement, gcc -O2 -ffp-contract=off -fopenmp, OpenMP {nt} threads, "
+                 f"schedule(dynamic,1) over rows): best of 3 blocks of whole {cfg.name} frames "
+                 f"({', '.join(str(b[0]) for b in pblocks)} frames in {', '.join(f'{b[1]:.1f}' for b in pblocks)} s)")
+    if os.path.exists(po.REF_SO):
+        try:
+            rgb = po.ref_render(scene, W, H, B, cam.pitch, nthreads=nt)
+            want = golden.manifest()["frames"].get(cfg.name, {}).get("fnv1a64")
+            ref_hash = f"{po.fnv1a64(rgb):016x}"
+            rblocks, rbest = cpu_sample(lambda: po.ref_render(scene, W, H, B, cam.pitch, nthreads=nt), args.cpu_seconds / 2)
+            val = rays_frame * rbest[0] / rbest[1] / 1e6
+            return {"value": round(val, 3), "kind": "reference", **common,
+                    "sample": f"best of 3 blocks of whole {cfg.name} frames ({W}x{H}, {rays_frame} rays each; blocks of "
+                              f"{', '.join(str(b[0]) for b in rblocks)} frames in "
+                              f"{', '.join(f'{b[1]:.1f}' for b in rblocks)} s) traced by the reference's own "
+                              f"rayTraceRay (Hw4/MySdlApplication.cpp:1184-1249 compiled from its sources, "
+                              f"oracle/_ref/libref.so, g++ -O2), OpenMP {nt} threads over rows; "
+                              f"{rbest[1] / rbest[0] * 1e3:.1f} ms/frame",
+                    "reference_frame_fnv1a64": ref_hash, "reference_frame_matches_golden": ref_hash == want,
+                    "port_value": round(port, 3), "port_sample": port_desc,
+                    "port_one_thread_value": round(per_core, 3)}
+        except Exception as exc:                             # reported; the port stands in
+            common["reference_error"] = f"{type(exc).__name__}: {exc}"
+    return {"value": round(port, 3), "kind": "port", **common,
+            "sample": f"{port_desc}; {pbest[1] / pbest[0] * 1e3:.1f} ms/frame",
+            "one_thread_value": round(per_core, 3),
+            "all_affinity_cores_linear_estimate": round(per_core * affinity_cores(), 3)}
 
 
 def torch_device_count() -> int:
@@ -893,39 +958,7 @@ def main() -> int:
     if rank == 0:
         res = result()
         if world == 1 and not args.no_cpu_baseline and not args.profile_kernel_only:
-            from oracle import pyoracle as po
-            nt = cpu_threads()
-            sa = scene.to_abi()
-            po.render(sa, cam, W, H, B, nthreads=nt)                 # warm (library load, page faults)
-            # best of 3 blocks of whole frames, each about --cpu-seconds / 3 of wall time
-            blocks = []
-            for _ in range(3):
-                n, t0c = 0, time.perf_counter()
-                while n < 1 or time.perf_counter() - t0c < args.cpu_seconds / 3:
-                    po.render(sa, cam, W, H, B, nthreads=nt)
-                    n += 1
-                blocks.append((n, time.perf_counter() - t0c))
-            best = max(blocks, key=lambda b: b[0] / b[1])
-            # one thread, for the per-core rate
-            n1, t1 = 0, time.perf_counter()
-            while n1 < 1 or time.perf_counter() - t1 < 2.0:
-                po.render(sa, cam, W, H, B, nthreads=1)
-                n1 += 1
-            t1 = time.perf_counter() - t1
-            per_core = rays_frame * n1 / t1 / 1e6
-            res["cpu_baseline"] = {
-                "value": round(rays_frame * best[0] / best[1] / 1e6, 3), "unit": "Mray/s", "cores": nt, "kind": "port",
-                "sample": f"best of 3 blocks of whole {cfg.name} frames ({W}x{H}, {rays_frame} rays each; "
-                          f"blocks of {', '.join(str(b[0]) for b in blocks)} frames in "
-                          f"{', '.join(f'{b[1]:.1f}' for b in blocks)} s) with oracle/rt_oracle.c (bit-exact "
-                          f"restatement, gcc -O2 -ffp-contract=off -fopenmp, OpenMP {nt} threads, "
-                          f"schedule(dynamic,1) over rows); {best[1] / best[0] * 1e3:.1f} ms/frame; host CPU: "
-                          f"{cpu_model()}",
-                "threads_used": nt, "nproc": os.cpu_count(), "affinity_cores": affinity_cores(),
-                "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
-                "one_thread_value": round(per_core, 3),
-                "all_affinity_cores_linear_estimate": round(per_core * affinity_cores(), 3),
-            }
+            res["cpu_baseline"] = cpu_baseline(args, cfg, scene, cam, W, H, B, rays_frame)
         print(json.dumps(res), file=out, flush=True)
     tr.close()
     if world > 1:

@@ -236,11 +236,13 @@ int rt_scene_achromatic(const rt_scene* scene, int* out);
 int rt_render_dev_packed(rt_ctx* ctx, const rt_camera* cam, int width, int height, int depth, const rt_rows* rows,
                          int float_format, void* float_pixels, int byte_format, void* byte_pixels, void* stream);
 /* Host-buffer frames in one format (draw()'s replacement with fewer PCIe bytes).  rt_render_packed is
- * synchronous (stats nullable, as rt_render).  rt_render_packed_async queues the render and the
- * device-to-host copy on the context's own streams and returns at once with a ticket; the copy of frame t
- * overlaps the render of frame t+1 (two device buffers); rt_ctx_wait(ctx, t) returns when frame t's pixels
- * are in host_pixels (ticket 0: everything queued).  host_pixels must stay valid until then; pinned memory
- * (rt_host_alloc) makes the copy a true DMA. */
+ * synchronous (stats nullable, as rt_render): the render and a copy kernel that writes the frame over PCIe
+ * into host_pixels, back to back on the context's render stream.  rt_render_packed_async queues the render
+ * on the render stream and the device-to-host copy as an SDMA transfer on the context's copy stream, and
+ * returns at once with a ticket: the copy of frame t runs beside the render of frame t+1 (three device
+ * buffers: up to two frames may be waited for behind the one being queued); rt_ctx_wait(ctx, t) returns
+ * when frame t's pixels are in host_pixels (ticket 0: everything queued).  host_pixels must stay valid until
+ * then; pinned memory (rt_host_alloc) makes the copy a true DMA. */
 int rt_render_packed(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, int width, int height, int depth,
                      int format, void* host_pixels, rt_stats* stats);
 int rt_render_packed_async(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, int width, int height,

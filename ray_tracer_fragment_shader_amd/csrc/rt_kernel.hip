@@ -370,11 +370,19 @@ struct rt_ctx {
                                                // than no bound: tools/ab.py); RT_MIN_WAVES=0 disables
     int use_lds = 0;                           // RT_SCENE_IN_LDS=1: header + exact records in LDS (A/B: tools/ab.py)
     int wg_staging = 0;                        // RT_WG_STAGING=1: LDS-staged 32-pixel row stores (A/B)
-    // RT_COPY_MODE (A/B): 1 (default) host copies queued behind the render on the render stream, 0 on the copy
-    // stream behind a cross-stream event.  Measured at c2 GRAY8 with copy kernels: synchronous 0.089 vs 0.100 ms
-    // per call, pipelined 0.079 either way (tools/packed_probe.py).
-    int copy_mode = 1;
-    int copy_kernel = 1;                       // RT_COPY_KERNEL=0: hipMemcpyAsync for rt_host_alloc memory too (A/B)
+    // Where the packed host frames' device-to-host copy runs (r04, tools/copy_ab.py and tools/copy_trace.py on MI355X,
+    // c2 GRAY8, 2.07 MB into pinned memory; us per frame):
+    //                                          synchronous   pipelined (wait f-1)   (wait f-2)
+    //   copy kernel behind the render (rs)         85              74                 74
+    //   copy kernel on the copy stream (cs)       100              75                 72   (16 workgroups: 66)
+    //   SDMA (hipMemcpyAsync) on the copy stream  107              59-60              59
+    // A copy kernel running beside the next render slows both (kernel trace: render 36 -> 60 us, copy 38 -> 55 us);
+    // the SDMA engines take no CUs.  So rt_render_packed (synchronous) queues a copy kernel behind the render on
+    // `rs`, and rt_render_packed_async an SDMA copy on `cs` after a cross-stream event.  RT_COPY_MODE (1: rs,
+    // 0: cs, 2: the kernel stores straight into the pinned buffer — 290 us: single-byte stores over PCIe) and
+    // RT_COPY_KERNEL (1: copy kernel, 0: SDMA) force one choice for both calls (A/B; -1: the defaults above).
+    int copy_mode = -1;
+    int copy_kernel = -1;
     int copy_blocks = 0;                       // RT_COPY_BLOCKS: workgroups of the copy kernel (0: one per 4 KB, <= 1024)
     // Adaptive tile-row order (rt_order_kernel): the first render of a new (scene, camera, size, rows,
     // depth, outputs) view uses the identity order; the second render of the same view is a calibration
@@ -430,6 +438,7 @@ struct rt_ctx {
     hipEvent_t rendered[kSlots] = {};          // slot b's packed frame is in its device buffer
     hipEvent_t copied[kSlots] = {};            // slot b's packed frame is in its host buffer
     bool copied_rec[kSlots] = {};
+    bool copied_cs[kSlots] = {};               // ... by a copy on the copy stream (else on the render stream)
     uint64_t ticket = 0;                       // rt_render_packed_async frames queued so far
     // rt_render's device buffers (grow-only, reused across calls): rgba32f, rgba8, rgb64f, raycount, sums,
     // packed slot 0, packed slot 1
@@ -513,9 +522,9 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_MIN_WAVES")) c->min_waves = atoi(e);
     if (const char* e = getenv("RT_WG_STAGING")) c->wg_staging = atoi(e) != 0;
     if (const char* e = getenv("RT_TILE_ORDER")) c->order_mode = atoi(e) == 1 ? 1 : 0;   // 1: bottom-to-top (A/B)
-    if (const char* e = getenv("RT_COPY_MODE")) c->copy_mode = std::min(std::max(atoi(e), 0), 2);
+    if (const char* e = getenv("RT_COPY_MODE")) c->copy_mode = std::min(std::max(atoi(e), -1), 2);
     if (const char* e = getenv("RT_COPY_BLOCKS")) c->copy_blocks = std::max(atoi(e), 0);
-    if (const char* e = getenv("RT_COPY_KERNEL")) c->copy_kernel = atoi(e) != 0;
+    if (const char* e = getenv("RT_COPY_KERNEL")) c->copy_kernel = std::min(std::max(atoi(e), -1), 1);
     if (const char* e = getenv("RT_CONE_CACHE")) c->cone_cache = atoi(e) != 0;
     if (hipMalloc(&c->d_tile_rows, sizeof(int32_t) * kOrderMax) != hipSuccess ||
         hipMalloc(&c->d_row_cost, sizeof(uint32_t) * kOrderMax) != hipSuccess) {
@@ -927,10 +936,12 @@ static void* pinned_device_ptr(const void* host, size_t bytes) {
     return (void*)(it->second.second + (h - it->first));
 }
 
-static int copy_to_host(rt_ctx* c, void* host, const void* dev, size_t bytes, hipStream_t st) {
+// kernel: copy kernel into rt_host_alloc memory (else hipMemcpyAsync); RT_COPY_KERNEL overrides.
+static int copy_to_host(rt_ctx* c, void* host, const void* dev, size_t bytes, hipStream_t st, bool kernel = true) {
     if (!bytes) return RT_OK;
     void* dmap = pinned_device_ptr(host, bytes);
-    if (dmap && c->copy_kernel && ((uintptr_t)dmap | (uintptr_t)dev) % 16 == 0) {
+    if (c->copy_kernel >= 0) kernel = c->copy_kernel != 0;
+    if (dmap && kernel && ((uintptr_t)dmap | (uintptr_t)dev) % 16 == 0) {
         unsigned blocks = (unsigned)std::min<size_t>((bytes / 16 + kThreads - 1) / kThreads + 1, 1024);
         if (c->copy_blocks > 0) blocks = std::min(blocks, (unsigned)c->copy_blocks);
         hipLaunchKernelGGL(rt_copy_out_kernel, dim3(blocks), dim3(kThreads), 0, st, (const uint8_t*)dev,
@@ -981,8 +992,11 @@ extern "C" int rt_render(rt_ctx* c, const rt_scene* scene, const rt_camera* cam,
 }
 
 // rt_render_packed / rt_render_packed_async: one image in `format`, copied to host memory.
+// async: the copy goes to the copy stream as an SDMA transfer (pipelined frames), else a copy kernel behind the
+// render on the render stream (see rt_ctx::copy_mode).
 static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera* cam, int W, int H, int depth,
-                               int format, void* host, int slot, bool with_stats, size_t* npx_out, void** sums) {
+                               int format, void* host, int slot, bool with_stats, size_t* npx_out, void** sums,
+                               bool async) {
     if (!c) return rt_fail(RT_EINVAL, "rt_render_packed: null context");
     if (!host) return rt_fail(RT_EINVAL, "rt_render_packed: null host buffer");
     int pb = 0;
@@ -1000,13 +1014,15 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
     void* rcb = nullptr;
     // RT_COPY_MODE=2 (A/B): the kernel stores the frame straight into the pinned host buffer (mapped into the
     // device's address space), no device buffer and no copy
-    void* direct = c->copy_mode == 2 ? pinned_device_ptr(host, npx * pb) : nullptr;
+    const int mode = c->copy_mode >= 0 ? c->copy_mode : (async ? 0 : 1);
+    void* direct = mode == 2 ? pinned_device_ptr(host, npx * pb) : nullptr;
     if (direct) px = direct;
     else if ((rc = ctx_buffer(c, 5 + slot, npx * pb, &px))) return rc;
     if (with_stats && ((rc = ctx_buffer(c, 3, npx * 4, &rcb)) || (rc = ctx_buffer(c, 4, 16, sums)))) return rc;
-    const hipStream_t cs = c->copy_mode != 0 ? c->rs : c->cs;
-    // the slot's device buffer is free once its previous frame's copy has left (stream-ordered on the GPU)
-    if (c->copied_rec[slot] && cs != c->rs) RT_HIP(hipStreamWaitEvent(c->rs, c->copied[slot], 0));
+    const hipStream_t cs = mode != 0 ? c->rs : c->cs;
+    // the slot's device buffer is free once its previous frame's copy has left (ordered by the stream when that
+    // copy ran on the render stream)
+    if (c->copied_rec[slot] && c->copied_cs[slot]) RT_HIP(hipStreamWaitEvent(c->rs, c->copied[slot], 0));
     if (with_stats) RT_HIP(hipEventRecord(c->ev0, c->rs));
     const bool f = float_format(format);
     rc = render_dev_impl(c, cam, W, H, depth, nullptr, f ? format : RT_PIXEL_RGBA32F, f ? px : nullptr,
@@ -1019,9 +1035,10 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
         RT_HIP(hipEventRecord(c->rendered[slot], c->rs));
         RT_HIP(hipStreamWaitEvent(cs, c->rendered[slot], 0));
     }
-    if (!direct && (rc = copy_to_host(c, host, px, npx * pb, cs))) return rc;
+    if (!direct && (rc = copy_to_host(c, host, px, npx * pb, cs, !async))) return rc;
     RT_HIP(hipEventRecord(c->copied[slot], cs));
     c->copied_rec[slot] = true;
+    c->copied_cs[slot] = cs != c->rs;
     return RT_OK;
 }
 
@@ -1032,7 +1049,7 @@ extern "C" int rt_render_packed(rt_ctx* c, const rt_scene* scene, const rt_camer
     if (!c) return rt_fail(RT_EINVAL, "rt_render_packed: null context");
     const uint64_t t = c->ticket + 1;                   // issued only once the frame is queued
     int rc = render_packed_queue(c, scene, cam, W, H, depth, format, host_pixels, (int)(t % rt_ctx::kSlots), stats != nullptr,
-                                 &npx, &sums);
+                                 &npx, &sums, false);
     if (rc) return rc;
     c->ticket = t;
     RT_HIP(hipEventSynchronize(c->copied[t % rt_ctx::kSlots]));
@@ -1050,7 +1067,7 @@ extern "C" int rt_render_packed_async(rt_ctx* c, const rt_scene* scene, const rt
     if (!c) return rt_fail(RT_EINVAL, "rt_render_packed_async: null context");
     const uint64_t t = c->ticket + 1;
     int rc = render_packed_queue(c, scene, cam, W, H, depth, format, host_pixels, (int)(t % rt_ctx::kSlots), false, &npx,
-                                 &sums);
+                                 &sums, true);
     if (rc) return rc;
     c->ticket = t;
     if (ticket) *ticket = t;
@@ -1075,7 +1092,9 @@ extern "C" int rt_ctx_wait(rt_ctx* c, uint64_t ticket) {
 extern "C" int rt_host_alloc(size_t bytes, void** out) {
     if (!out || bytes == 0) return rt_fail(RT_EINVAL, "rt_host_alloc: bad arguments");
     *out = nullptr;
-    RT_HIP(hipHostMalloc(out, bytes, hipHostMallocDefault));
+    // RT_HOST_NONCOHERENT=1 (A/B): non-coherent pinned memory (the GPU may cache its writes until the kernel ends)
+    const char* nc = getenv("RT_HOST_NONCOHERENT");
+    RT_HIP(hipHostMalloc(out, bytes, nc && atoi(nc) ? hipHostMallocNonCoherent : hipHostMallocDefault));
     void* dmap = nullptr;
     if (hipHostGetDevicePointer(&dmap, *out, 0) != hipSuccess || !dmap) dmap = nullptr;
     if (dmap) {                                         // host frames in it are copied by rt_copy_out_kernel

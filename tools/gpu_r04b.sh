@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$(pwd)/gpurun_out
 mkdir -p "$OUT"
-want() { case " ${STEPS:-tests slots ab ctrace bench} " in *" $1 "*) return 0;; esac; return 1; }
+want() { case " ${STEPS:-tests ab bench copy2} " in *" $1 "*) return 0;; esac; return 1; }
 if want tests; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} \
       > "$OUT/gpu_tests.log" 2>&1
@@ -36,4 +36,11 @@ if want ctrace; then
     cat "$OUT/ctrace_$1_$2_$3.json"; python3 "$GRAFT_REPO_ROOT/tools/copy_trace.py" parse "$OUT/ctrace_$1_$2_$3"
   done
   cd "$GRAFT_REPO_ROOT"
+fi
+if want copy2; then
+  for env in "RT_HOST_NONCOHERENT=0" "RT_HOST_NONCOHERENT=1" "RT_COPY_KERNEL=0"; do
+    env $env SETTINGS=1:0,0:16,0:0 ROUNDS=3 timeout -k 10 200 python -u tools/copy_ab.py > "$OUT/copy2_$env.json" \
+        2> "$OUT/copy2_$env.err" || { echo "copy2 $env failed"; tail -5 "$OUT/copy2_$env.err"; exit 8; }
+    echo "$env"; python3 -c "import json; print(json.load(open('$OUT/copy2_$env.json'))['us_per_frame_median'])"
+  done
 fi
