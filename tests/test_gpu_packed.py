@@ -301,6 +301,47 @@ def test_render_packed_host_sync_and_async(tr):
         t.close()
 
 
+def test_render_packed_two_behind_and_mixed_sync(tr):
+    """rt_render_packed_async with two frames waited for behind the one being queued (three pinned buffers, the
+    SDMA copies on the copy stream), interleaved with synchronous rt_render_packed calls (copy kernel on the render
+    stream) that reuse the same device slots: every frame, waited for by its ticket, equals the device render."""
+    L = abi.lib()
+    cfg = scenes.CONFIGS["c2"]
+    sa = cfg.scene().to_abi()
+    W, H = 640, 360
+    cams = [cfg.camera(W, H) for _ in range(3)]
+    cams[1].eye = abi.vec3((-40.0, 120.0, 230.0))
+    cams[2].eye = abi.vec3((35.0, 90.0, 210.0))
+    tr.set_scene(cfg.scene())
+    want = [_rgba(tr, c, W, H, cfg.depth)[1].cpu().numpy()[..., 0] for c in cams]
+    t = Tracer(0)
+    pins = [_host_alloc(W * H) for _ in range(4)]
+    try:
+        tickets = []
+        for f in range(12):
+            tk = ctypes.c_uint64()
+            abi.check(L.rt_render_packed_async(t._ctx, ctypes.byref(sa), ctypes.byref(cams[f % 3]), W, H, cfg.depth,
+                                               P.RT_PIXEL_GRAY8, pins[f % 3], ctypes.byref(tk)), "async")
+            tickets.append(tk.value)
+            if f % 4 == 3:                               # a synchronous frame in between (render-stream copy)
+                abi.check(L.rt_render_packed(t._ctx, ctypes.byref(sa), ctypes.byref(cams[(f + 1) % 3]), W, H,
+                                             cfg.depth, P.RT_PIXEL_GRAY8, pins[3], None), "rt_render_packed")
+                got = np.ctypeslib.as_array(ctypes.cast(pins[3], ctypes.POINTER(ctypes.c_uint8)), (H, W))
+                assert np.array_equal(got, want[(f + 1) % 3]), f"sync after {f}"
+            if f >= 2:
+                abi.check(L.rt_ctx_wait(t._ctx, tickets[f - 2]), "rt_ctx_wait")
+                got = np.ctypeslib.as_array(ctypes.cast(pins[(f - 2) % 3], ctypes.POINTER(ctypes.c_uint8)), (H, W))
+                assert np.array_equal(got, want[(f - 2) % 3]), f - 2
+        abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
+        for f in (10, 11):
+            got = np.ctypeslib.as_array(ctypes.cast(pins[f % 3], ctypes.POINTER(ctypes.c_uint8)), (H, W))
+            assert np.array_equal(got, want[f % 3]), f
+    finally:
+        for p in pins:
+            L.rt_host_free(p)
+        t.close()
+
+
 def test_hits_inside_shortcut_far_origins(tr):
     """Rays from hit points skip the bounding-sphere cull only when the host proved every hit point lies inside
     its shortcut radius with a slack that covers the hit point's rounding, which grows with the level-0 origin's

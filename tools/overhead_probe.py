@@ -35,7 +35,7 @@ for _ in range(30):
     for a in la:
         fn(*a)
 torch.cuda.synchronize()
-res = {"sync": [], "spin": [], "interval": [], "host_call_us": [], "first_start_us": []}
+res = {"sync": [], "spin": [], "nowait": [], "interval": [], "interval_nowait": [], "host_call_us": []}
 K = int(os.environ.get("K", "20"))
 for rnd in range(15):
     t_end = time.perf_counter() + 0.1
@@ -70,4 +70,17 @@ for rnd in range(15):
         res[mode].append(wall / K * 1e6)
         res["interval"].append(ev0.elapsed_time(ev1) / K * 1e3)
         res["host_call_us"].append(t_call * 1e6)
+    # bench.py r04: no cross-stream waits in the region, an end stamp per stream
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ends = [torch.cuda.Event(enable_timing=True) for _ in sts]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(sts[0])
+    for i in range(K):
+        fn(*la[i % nf])
+    for e, s in zip(ends, sts):
+        e.record(s)
+    torch.cuda.synchronize()
+    res["nowait"].append((time.perf_counter() - t0) / K * 1e6)
+    res["interval_nowait"].append(max(ev0.elapsed_time(e) for e in ends) / K * 1e3)
 print(json.dumps({k: round(statistics.median(v), 2) for k, v in res.items() if v} | {"K": K}))
