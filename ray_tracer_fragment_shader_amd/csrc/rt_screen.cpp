@@ -174,33 +174,55 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // chunk's randomUnit() values (rt_screen_form_ends): the host generates each stream value once and sends
     // 24 bytes per value instead of the rays.  Simulated on the reference's own sample counts (demo frame):
     // 759 round trips instead of 2,515, for ~85 traced samples per pixel instead of 7.
+    //
+    // Two chunks in flight (r04).  While the GPU traces chunk c, the host builds and queues chunk c + 1 as the
+    // continuation of c's prediction chain (the pixels below it that lie in c use c's predicted counts; its
+    // stream base is c's predicted end minus kWin), then waits for c and resolves it.  When c resolves to its
+    // end, c + 1 is already traced or tracing: the host's build and resolution overlap the GPU's round trip
+    // instead of following it.  When c breaks, c + 1 is dropped (its buffers are reused once the stream has
+    // passed it) and a chunk starts at the break, as before.  Resolution is unchanged: every pixel reads its
+    // samples at its actual stream position, or breaks.
     const int kMaxRays = 1 << 19, kMaxPix = 4096, kWin = 28;
     const int kMaxJit = kMaxPix * 16 + 2 * kWin + 16;
     static_assert(16 + 2 * kWin <= kScreenMaxWindow, "window exceeds the ray-formation workgroup");
-    DevBuf d_start, d_end;
-    HostBuf h_rgb, h_pix, h_jit;
-    void* d_rgb = nullptr;
-    void* d_pix = nullptr;
-    void* d_jit = nullptr;
+    struct Buf {                                                     // one chunk's device / mapped buffers
+        DevBuf d_end;
+        HostBuf h_rgb, h_pix, h_jit;
+        void* d_rgb = nullptr;
+        void* d_pix = nullptr;
+        void* d_jit = nullptr;
+        hipEvent_t done = nullptr;                                   // recorded after the chunk's trace
+        ~Buf() {
+            if (done) (void)hipEventDestroy(done);
+        }
+    };
+    DevBuf d_start;
+    Buf buf[2];
     Stream st;
     const size_t ray_bytes = (size_t)kMaxRays * 3 * sizeof(double);
     const unsigned mapped = hipHostMallocMapped | hipHostMallocCoherent;
     hipError_t e = hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&d_start.p, ray_bytes);
-    if (e == hipSuccess) e = hipMalloc(&d_end.p, ray_bytes);
-    if (e == hipSuccess) e = hipHostMalloc(&h_rgb.p, ray_bytes, mapped);
-    if (e == hipSuccess) e = hipHostMalloc(&h_pix.p, (size_t)kMaxPix * sizeof(ScreenPix), mapped);
-    if (e == hipSuccess) e = hipHostMalloc(&h_jit.p, (size_t)kMaxJit * 3 * sizeof(double), mapped);
-    if (e == hipSuccess) e = hipHostGetDevicePointer(&d_rgb, h_rgb.p, 0);
-    if (e == hipSuccess) e = hipHostGetDevicePointer(&d_pix, h_pix.p, 0);
-    if (e == hipSuccess) e = hipHostGetDevicePointer(&d_jit, h_jit.p, 0);
+    for (Buf& b : buf) {
+        if (e == hipSuccess) e = hipMalloc(&b.d_end.p, ray_bytes);
+        if (e == hipSuccess) e = hipHostMalloc(&b.h_rgb.p, ray_bytes, mapped);
+        if (e == hipSuccess) e = hipHostMalloc(&b.h_pix.p, (size_t)kMaxPix * sizeof(ScreenPix), mapped);
+        if (e == hipSuccess) e = hipHostMalloc(&b.h_jit.p, (size_t)kMaxJit * 3 * sizeof(double), mapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_rgb, b.h_rgb.p, 0);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_pix, b.h_pix.p, 0);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_jit, b.h_jit.p, 0);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
+    }
     if (e != hipSuccess) return rt_fail(RT_ENOMEM, std::string("rt_render_screen: ") + hipGetErrorString(e));
+    struct Drain {                                                   // on every return: the stream's work is done
+        hipStream_t s;                                               // before the buffers above are freed
+        ~Drain() {
+            if (s) (void)hipStreamSynchronize(s);
+        }
+    } drain{st.s};
     const double cam_p[3] = {camera.x, camera.y, camera.z};
     rc = rt_fill_points(static_cast<double*>(d_start.p), kMaxRays, cam_p, st.s);
     if (rc) return rc;
-    const double* hr = static_cast<const double*>(h_rgb.p);
-    ScreenPix* hp = static_cast<ScreenPix*>(h_pix.p);
-    double* hj = static_cast<double*>(h_jit.p);
 
     Jitter jit(rand_kind, seed);
     V3 avgColor = v3(0.0, 0.0, 0.0);                                 // :1283, carried across pixels
@@ -209,29 +231,55 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     uint64_t S = 0;                                                  // its first sample in the stream
     int chunk = 64;
     std::vector<uint8_t> counts((size_t)P, 0);                       // resolved sample counts (predictions)
-    std::vector<V3> sp(kMaxPix);
-    // RT_SCREEN_PROFILE=1: host build / GPU round trip / resolve times and chunk counts on stderr.
+    std::vector<uint8_t> pcount((size_t)P, 0);                       // predicted counts of queued pixels
+    // RT_SCREEN_PROFILE=1: host build / GPU wait / resolve times and chunk counts on stderr.
     const bool prof = getenv("RT_SCREEN_PROFILE") != nullptr;
+    // RT_SCREEN_NEXT (A/B): size of the queued continuation as a multiple of the current chunk size (0: none, one
+    // chunk in flight as in r03).
+    int next_mul = 2;
+    if (const char* ev = getenv("RT_SCREEN_NEXT")) next_mul = std::max(0, atoi(ev));
     using clk = std::chrono::steady_clock;
     double t_build = 0, t_gpu = 0, t_res = 0;
-    long long n_chunks = 0, n_rays = 0;
-    while (p < P) {
+    long long n_chunks = 0, n_rays = 0, n_dropped = 0;
+
+    // A queued chunk: pixels p0 .. p0+m-1, windows relative to stream index S0.
+    struct Chunk {
+        int b = 0;                                                   // buffer set
+        long long p0 = 0;
+        int m = 0;
+        uint64_t S0 = 0;
+        long long spred_end = 0;                                     // predicted start of pixel p0+m, rel. to S0
+        uint64_t jend = 0;                                           // its stream values: S0 .. jend - 1
+        V3 walk_end = v3(0.0, 0.0, 0.0);                             // screen point of pixel p0+m
+        std::vector<V3> sp;                                          // screen point of each pixel
+    };
+    // Build chunk (pixels p0.., at most `want`) into buffer set b and queue its round trip.  pred_start: the
+    // predicted first sample of pixel p0 (absolute); the chunk's base is pred_start - kWin, at least `floor`.
+    auto queue = [&](Chunk& c, int b, long long p0, uint64_t pred_start, uint64_t floor, V3 w0, int want) -> int {
         const auto c0 = clk::now();
-        // Chunk: pixels p .. p+m-1 with their predicted counts and sample windows.
-        int m = (int)std::min<long long>(chunk, P - p);
-        V3 w = walk;
+        Buf& B = buf[b];
+        ScreenPix* hp = static_cast<ScreenPix*>(B.h_pix.p);
+        double* hj = static_cast<double*>(B.h_jit.p);
+        c.b = b;
+        c.p0 = p0;
+        c.S0 = std::max<uint64_t>(floor, pred_start > (uint64_t)kWin ? pred_start - kWin : 0);
+        c.sp.resize(kMaxPix);
+        int m = (int)std::min<long long>(want, P - p0);
+        V3 w = w0;
         int total = 0, jmax = 0;
-        long long spred = 0;                                         // predicted first sample, relative to S
+        long long spred = (long long)pred_start - (long long)c.S0;  // predicted first sample, relative to S0
         for (int q = 0; q < m; ++q) {
-            const long long pix = p + q;
-            const int pred = (pix - W >= 0 && pix - W < p) ? counts[pix - W] : (p > 0 ? counts[p - 1] : 16);
-            const long long lo = std::max(0LL, spred - kWin), hi = spred + pred + kWin;
+            const long long pix = p0 + q;
+            const long long below = pix - W;
+            const int pred = below >= 0 ? (below < p ? counts[below] : pcount[below]) : (p > 0 ? counts[p - 1] : 16);
+            const long long lo = std::max(0LL, spred - kWin), hi = std::max(lo, spred + pred + kWin);
             const int len = (int)(hi - lo);
             if (total + len > kMaxRays || hi > kMaxJit) {
                 m = q;
                 break;
             }
-            sp[q] = w;
+            pcount[pix] = (uint8_t)pred;
+            c.sp[q] = w;
             hp[q].sp[0] = w.x, hp[q].sp[1] = w.y, hp[q].sp[2] = w.z;
             hp[q].base = (int32_t)lo, hp[q].len = len, hp[q].off = total, hp[q].pad = 0;
             total += len;
@@ -240,30 +288,56 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
             w = w + right;                                           // screenPt += right (:1315)
             if ((int)(pix % W) == W - 1) w = (w - rightOffset) + up; // :1320-1321
         }
-        for (int k = 0; k < jmax; ++k) {                             // randomUnit() values S .. S + jmax - 1
-            const V3& v = jit.at(S + (uint64_t)k);
+        c.m = m;
+        c.spred_end = spred;
+        c.jend = c.S0 + (uint64_t)jmax;
+        c.walk_end = w;
+        for (int k = 0; k < jmax; ++k) {                             // randomUnit() values S0 .. S0 + jmax - 1
+            const V3& v = jit.at(c.S0 + (uint64_t)k);
             hj[3 * k] = v.x, hj[3 * k + 1] = v.y, hj[3 * k + 2] = v.z;
         }
-        const auto c1 = clk::now();
-        // One round trip: form the rays, trace them (colours straight into host memory), synchronise.
-        rc = rt_screen_form_ends(static_cast<const ScreenPix*>(d_pix), m, static_cast<const double*>(d_jit),
-                                 static_cast<double*>(d_end.p), st.s);
-        if (rc) return rc;
-        rc = rt_trace_rays_dev(ctx, static_cast<const double*>(d_start.p), static_cast<const double*>(d_end.p), total,
-                               depth, static_cast<double*>(d_rgb), nullptr, st.s);
-        if (rc) return rc;
-        // While the GPU traces: generate the stream values the next chunk will need (rand() + normalize are
-        // the host's largest share of a round trip), so its build only copies them.
-        (void)jit.at(S + 2 * (uint64_t)jmax + 64);
-        e = hipStreamSynchronize(st.s);
-        if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(e));
+        // One round trip: form the rays, trace them (colours straight into host memory).
+        int r = rt_screen_form_ends(static_cast<const ScreenPix*>(B.d_pix), m, static_cast<const double*>(B.d_jit),
+                                    static_cast<double*>(B.d_end.p), st.s);
+        if (!r) r = rt_trace_rays_dev(ctx, static_cast<const double*>(d_start.p), static_cast<const double*>(B.d_end.p),
+                                      total, depth, static_cast<double*>(B.d_rgb), nullptr, st.s);
+        if (r) return r;
+        const hipError_t er = hipEventRecord(B.done, st.s);
+        if (er != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(er));
+        if (prof) {
+            t_build += std::chrono::duration<double>(clk::now() - c0).count();
+            ++n_chunks;
+            n_rays += total;
+        }
+        return RT_OK;
+    };
 
+    Chunk cur, nxt;
+    if ((rc = queue(cur, 0, 0, 0, 0, walk, chunk))) return rc;
+    while (p < P) {
+        // the continuation of cur's prediction chain, queued behind it
+        bool have_next = false;
+        if (next_mul > 0 && cur.p0 + cur.m < P) {
+            if ((rc = queue(nxt, cur.b ^ 1, cur.p0 + cur.m, cur.S0 + (uint64_t)cur.spred_end, S, cur.walk_end,
+                            std::min(chunk * next_mul, kMaxPix))))
+                return rc;
+            have_next = true;
+        }
+        // While the GPU traces: generate the stream values the following chunk will need (rand() + normalize
+        // are the host's largest share of a round trip), so its build only copies them.
+        (void)jit.at(have_next ? nxt.jend + (nxt.jend - nxt.S0) + 64 : cur.jend + 64);
+        const auto c1 = clk::now();
+        e = hipEventSynchronize(buf[cur.b].done);
+        if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(e));
         const auto c2 = clk::now();
-        // Resolve in order with the reference's loop (:1294-1311), each sample read from its pixel's window.
+
+        // Resolve cur in order with the reference's loop (:1294-1311), each sample read from its pixel's window.
+        const double* hr = static_cast<const double*>(buf[cur.b].h_rgb.p);
+        const ScreenPix* hp = static_cast<const ScreenPix*>(buf[cur.b].h_pix.p);
         int q = 0;
-        long long A = 0;                                             // actual first sample of pixel q, relative to S
-        bool broke = false;
-        for (; q < m; ++q) {
+        long long A = (long long)S - (long long)cur.S0;               // actual first sample of pixel q, rel. to S0
+        bool broke = A < 0;
+        for (; q < cur.m && !broke; ++q) {
             const ScreenPix& X = hp[q];
             if (A < X.base) {                                        // the stream ran behind the window
                 broke = true;
@@ -290,7 +364,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
                 break;
             }
             avgColor = v3(avgColor.x / k, avgColor.y / k, avgColor.z / k);   // avgColor /= k (:1310)
-            const long long pix = p + q;
+            const long long pix = cur.p0 + q;
             if (rgb64f) {
                 rgb64f[3 * pix] = avgColor.x, rgb64f[3 * pix + 1] = avgColor.y, rgb64f[3 * pix + 2] = avgColor.z;
             }
@@ -301,26 +375,39 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
             if (samples) samples[pix] = (uint8_t)n;
             counts[pix] = (uint8_t)n;
             A += n;
-            walk = sp[q] + right;
+            walk = cur.sp[q] + right;
             if ((int)(pix % W) == W - 1) walk = (walk - rightOffset) + up;
         }
-        // (q >= 1: pixel p's window starts at its own first sample and holds >= 16 + kWin samples)
-        p += q;
-        S += (uint64_t)A;
+        p = cur.p0 + q;
+        if (q > 0) S = cur.S0 + (uint64_t)A;                         // (q == 0: nothing resolved, S unchanged)
         jit.consume_until(S);
-        chunk = broke ? std::max(16, chunk / 2) : std::min(kMaxPix, chunk * 2);
         if (prof) {
-            const auto c3 = clk::now();
-            t_build += std::chrono::duration<double>(c1 - c0).count();
             t_gpu += std::chrono::duration<double>(c2 - c1).count();
-            t_res += std::chrono::duration<double>(c3 - c2).count();
-            ++n_chunks;
-            n_rays += total;
+            t_res += std::chrono::duration<double>(clk::now() - c2).count();
+        }
+        if (!broke && q == cur.m) {
+            chunk = std::min(kMaxPix, chunk * 2);
+            if (have_next) {
+                std::swap(cur, nxt);                                 // already queued at the right place
+            } else if (p < P && (rc = queue(cur, cur.b, p, S, S, walk, chunk))) {
+                return rc;
+            }
+            continue;
+        }
+        // cur broke at pixel p: restart the chain there (in cur's buffers, free now) and drop the queued
+        // continuation, whose buffers the next continuation rewrites once the stream has passed it
+        chunk = std::max(16, chunk / 2);
+        const int dropped = have_next ? nxt.b : -1;
+        if (p < P && (rc = queue(cur, cur.b, p, S, S, walk, chunk))) return rc;
+        if (dropped >= 0) {
+            ++n_dropped;
+            e = hipEventSynchronize(buf[dropped].done);
+            if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(e));
         }
     }
     if (prof)
-        fprintf(stderr, "rt_render_screen: %lld chunks, %lld rays traced; build %.1f ms, gpu %.1f ms, resolve %.1f ms\n",
-                n_chunks, n_rays, t_build * 1e3, t_gpu * 1e3, t_res * 1e3);
+        fprintf(stderr, "rt_render_screen: %lld chunks (%lld dropped), %lld rays traced; build %.1f ms, gpu wait %.1f ms, "
+                "resolve %.1f ms\n", n_chunks, n_dropped, n_rays, t_build * 1e3, t_gpu * 1e3, t_res * 1e3);
     if (rand_calls) *rand_calls = jit.consumed_calls;
     return RT_OK;
 }

@@ -30,6 +30,16 @@ hipError_t hipStreamDestroy(hipStream_t s) {
     return hipSuccess;
 }
 hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned int) {
+    *e = reinterpret_cast<hipEvent_t>(new int(0));
+    return hipSuccess;
+}
+hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventDestroy(hipEvent_t e) {
+    delete reinterpret_cast<int*>(e);
+    return hipSuccess;
+}
 hipError_t hipMalloc(void** p, size_t n) {
     *p = std::malloc(n);
     return *p ? hipSuccess : hipErrorOutOfMemory;
