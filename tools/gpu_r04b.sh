@@ -44,3 +44,15 @@ if want copy2; then
     echo "$env"; python3 -c "import json; print(json.load(open('$OUT/copy2_$env.json'))['us_per_frame_median'])"
   done
 fi
+if want over; then
+  timeout -k 10 120 python -u tools/overhead_probe.py > "$OUT/overhead.json" 2> "$OUT/overhead.err" \
+      || { echo "overhead probe failed"; tail -20 "$OUT/overhead.err"; exit 13; }
+  cat "$OUT/overhead.json"
+fi
+if want screen; then
+  for n in 0 1 2; do
+    RT_SCREEN_NEXT=$n RT_SCREEN_PROFILE=1 timeout -k 10 200 python -u tools/screen_bench.py demo 500 500 c2 640 360 \
+        > "$OUT/screen_$n.json" 2> "$OUT/screen_$n.err" || { echo "screen $n failed"; tail -5 "$OUT/screen_$n.err"; exit 9; }
+    echo "RT_SCREEN_NEXT=$n"; cat "$OUT/screen_$n.json"; grep rt_render_screen "$OUT/screen_$n.err" | tail -2
+  done
+fi
