@@ -47,6 +47,11 @@ struct ScreenPix {
     int32_t base, len, off, pad;
 };
 constexpr int kScreenMaxWindow = 128;          // len <= this (one workgroup per pixel)
+constexpr int kScreenMaxRays = 1 << 19;        // rays of one chunk
+constexpr int kScreenMaxPix = 4096;            // pixels of one chunk
+constexpr int kScreenMaxJit = kScreenMaxPix * 16 + 128;   // stream values of one chunk
+// Frees the rt_render_screen buffers kept for `ctx` (rt_ctx_destroy).
+void rt_screen_release(const rt_ctx* ctx);
 // ends[off + j] = sp + 0.5 * jit[base + j] for every pixel of `pix` (device-visible), j < len (MSA:1296).
 int rt_screen_form_ends(const ScreenPix* pix, int m, const double* jit, double* ends, void* stream);
 // out[k] = p for k < n (the rays' common start, the camera).

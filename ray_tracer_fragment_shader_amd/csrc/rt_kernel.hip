@@ -486,6 +486,7 @@ extern "C" int rt_device_count(int* count) {
 extern "C" int rt_ctx_destroy(rt_ctx* c) {
     if (!c) return RT_OK;
     (void)hipSetDevice(c->device);
+    rt_screen_release(c);
     if (c->rs) (void)hipStreamSynchronize(c->rs);
     if (c->cs) (void)hipStreamSynchronize(c->cs);
     if (c->d_scene) (void)hipFree(c->d_scene);

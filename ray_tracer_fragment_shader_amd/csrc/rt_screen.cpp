@@ -27,7 +27,10 @@
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/rt_api.h"
@@ -143,7 +146,77 @@ struct Stream {
     }
 };
 
+struct ScreenBuf {                                                    // one chunk's device / mapped buffers
+    DevBuf d_end;
+    HostBuf h_rgb, h_pix, h_jit;
+    void* d_rgb = nullptr;
+    void* d_pix = nullptr;
+    void* d_jit = nullptr;
+    hipEvent_t done = nullptr;                                       // recorded after the chunk's trace
+    ~ScreenBuf() {
+        if (done) (void)hipEventDestroy(done);
+    }
+};
+struct ScreenWs {                                                    // two chunks in flight + the rays' start
+    Stream st;
+    DevBuf d_start;
+    ScreenBuf buf[2];
+};
+
+std::unique_ptr<ScreenWs> alloc_ws() {
+    std::unique_ptr<ScreenWs> w(new ScreenWs());
+    const size_t ray_bytes = (size_t)kScreenMaxRays * 3 * sizeof(double);
+    const unsigned mapped = hipHostMallocMapped | hipHostMallocCoherent;
+    hipError_t e = hipStreamCreateWithFlags(&w->st.s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&w->d_start.p, ray_bytes);
+    for (ScreenBuf& b : w->buf) {
+        if (e == hipSuccess) e = hipMalloc(&b.d_end.p, ray_bytes);
+        if (e == hipSuccess) e = hipHostMalloc(&b.h_rgb.p, ray_bytes, mapped);
+        if (e == hipSuccess) e = hipHostMalloc(&b.h_pix.p, (size_t)kScreenMaxPix * sizeof(ScreenPix), mapped);
+        if (e == hipSuccess) e = hipHostMalloc(&b.h_jit.p, (size_t)kScreenMaxJit * 3 * sizeof(double), mapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_rgb, b.h_rgb.p, 0);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_pix, b.h_pix.p, 0);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_jit, b.h_jit.p, 0);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
+    }
+    if (e != hipSuccess) return nullptr;
+    return w;
+}
+
+std::mutex g_ws_mu;
+std::unordered_map<const rt_ctx*, std::unique_ptr<ScreenWs>> g_ws;  // idle workspaces by context
+
+std::unique_ptr<ScreenWs> take_ws(const rt_ctx* ctx) {
+    {
+        std::lock_guard<std::mutex> lk(g_ws_mu);
+        auto it = g_ws.find(ctx);
+        if (it != g_ws.end() && it->second) {
+            std::unique_ptr<ScreenWs> w = std::move(it->second);
+            g_ws.erase(it);
+            return w;
+        }
+    }
+    return alloc_ws();
+}
+
+void give_ws(const rt_ctx* ctx, std::unique_ptr<ScreenWs> w) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    auto& slot = g_ws[ctx];
+    if (!slot) slot = std::move(w);                                  // else: freed here (a concurrent call's)
+}
+
 }  // namespace
+
+void rt_screen_release(const rt_ctx* ctx) {
+    std::unique_ptr<ScreenWs> w;
+    {
+        std::lock_guard<std::mutex> lk(g_ws_mu);
+        auto it = g_ws.find(ctx);
+        if (it == g_ws.end()) return;
+        w = std::move(it->second);
+        g_ws.erase(it);
+    }
+}
 
 extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, int W, int H, int depth,
                                 int rand_kind, uint32_t seed, double* rgb64f, uint8_t* rgba8, uint8_t* samples,
@@ -182,44 +255,27 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // instead of following it.  When c breaks, c + 1 is dropped (its buffers are reused once the stream has
     // passed it) and a chunk starts at the break, as before.  Resolution is unchanged: every pixel reads its
     // samples at its actual stream position, or breaks.
-    const int kMaxRays = 1 << 19, kMaxPix = 4096, kWin = 28;
-    const int kMaxJit = kMaxPix * 16 + 2 * kWin + 16;
+    const int kMaxRays = kScreenMaxRays, kMaxPix = kScreenMaxPix, kWin = 28;
+    const int kMaxJit = kScreenMaxJit;
     static_assert(16 + 2 * kWin <= kScreenMaxWindow, "window exceeds the ray-formation workgroup");
-    struct Buf {                                                     // one chunk's device / mapped buffers
-        DevBuf d_end;
-        HostBuf h_rgb, h_pix, h_jit;
-        void* d_rgb = nullptr;
-        void* d_pix = nullptr;
-        void* d_jit = nullptr;
-        hipEvent_t done = nullptr;                                   // recorded after the chunk's trace
-        ~Buf() {
-            if (done) (void)hipEventDestroy(done);
+    static_assert(kScreenMaxJit >= kScreenMaxPix * 16 + 2 * kWin + 16, "stream-value buffer too small");
+    // The buffers live in the context between calls (allocating ~40 MB of device and mapped host memory
+    // per frame cost more than a quarter of a demo frame); a call running concurrently on the same context
+    // allocates its own.
+    std::unique_ptr<ScreenWs> ws = take_ws(ctx);
+    if (!ws) return rt_fail(RT_ENOMEM, "rt_render_screen: workspace allocation failed");
+    struct Give {                                                    // on every return: the stream's work is
+        rt_ctx* ctx;                                                 // done, then the workspace goes back
+        std::unique_ptr<ScreenWs>& ws;
+        ~Give() {
+            (void)hipStreamSynchronize(ws->st.s);
+            give_ws(ctx, std::move(ws));
         }
-    };
-    DevBuf d_start;
-    Buf buf[2];
-    Stream st;
-    const size_t ray_bytes = (size_t)kMaxRays * 3 * sizeof(double);
-    const unsigned mapped = hipHostMallocMapped | hipHostMallocCoherent;
-    hipError_t e = hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(&d_start.p, ray_bytes);
-    for (Buf& b : buf) {
-        if (e == hipSuccess) e = hipMalloc(&b.d_end.p, ray_bytes);
-        if (e == hipSuccess) e = hipHostMalloc(&b.h_rgb.p, ray_bytes, mapped);
-        if (e == hipSuccess) e = hipHostMalloc(&b.h_pix.p, (size_t)kMaxPix * sizeof(ScreenPix), mapped);
-        if (e == hipSuccess) e = hipHostMalloc(&b.h_jit.p, (size_t)kMaxJit * 3 * sizeof(double), mapped);
-        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_rgb, b.h_rgb.p, 0);
-        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_pix, b.h_pix.p, 0);
-        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_jit, b.h_jit.p, 0);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
-    }
-    if (e != hipSuccess) return rt_fail(RT_ENOMEM, std::string("rt_render_screen: ") + hipGetErrorString(e));
-    struct Drain {                                                   // on every return: the stream's work is done
-        hipStream_t s;                                               // before the buffers above are freed
-        ~Drain() {
-            if (s) (void)hipStreamSynchronize(s);
-        }
-    } drain{st.s};
+    } give{ctx, ws};
+    DevBuf& d_start = ws->d_start;
+    ScreenBuf* buf = ws->buf;
+    Stream& st = ws->st;
+    hipError_t e = hipSuccess;
     const double cam_p[3] = {camera.x, camera.y, camera.z};
     rc = rt_fill_points(static_cast<double*>(d_start.p), kMaxRays, cam_p, st.s);
     if (rc) return rc;
@@ -236,7 +292,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     const bool prof = getenv("RT_SCREEN_PROFILE") != nullptr;
     // RT_SCREEN_NEXT (A/B): size of the queued continuation as a multiple of the current chunk size (0: none, one
     // chunk in flight as in r03).
-    int next_mul = 2;
+    int next_mul = 1;
     if (const char* ev = getenv("RT_SCREEN_NEXT")) next_mul = std::max(0, atoi(ev));
     using clk = std::chrono::steady_clock;
     double t_build = 0, t_gpu = 0, t_res = 0;
@@ -257,7 +313,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // predicted first sample of pixel p0 (absolute); the chunk's base is pred_start - kWin, at least `floor`.
     auto queue = [&](Chunk& c, int b, long long p0, uint64_t pred_start, uint64_t floor, V3 w0, int want) -> int {
         const auto c0 = clk::now();
-        Buf& B = buf[b];
+        ScreenBuf& B = buf[b];
         ScreenPix* hp = static_cast<ScreenPix*>(B.h_pix.p);
         double* hj = static_cast<double*>(B.h_jit.p);
         c.b = b;

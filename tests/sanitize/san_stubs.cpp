@@ -77,6 +77,7 @@ extern "C" int rt_ctx_create(int, rt_ctx** out) {
     return RT_OK;
 }
 extern "C" int rt_ctx_destroy(rt_ctx* c) {
+    rt_screen_release(c);
     delete c;
     return RT_OK;
 }

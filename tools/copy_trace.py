@@ -56,6 +56,10 @@ def parse(d):
                   if "rt_render_kernel" in r["Kernel_Name"]])[-30:]
     cop = sorted([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
                   if "rt_copy_out_kernel" in r["Kernel_Name"]])[-30:]
+    mc = glob.glob(d + "/**/*memory_copy_trace.csv", recursive=True)
+    if not cop and mc:                                       # SDMA copies (--memory-copy-trace)
+        cop = sorted([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(mc[0]))
+                      if "DEVICE_TO_HOST" in r.get("Direction", "")])[-30:]
     lo = max(ren[0][0], cop[0][0])
     ren = [x for x in ren if x[0] >= lo]
     cop = [x for x in cop if x[0] >= lo]

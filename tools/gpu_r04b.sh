@@ -27,10 +27,11 @@ if want bench; then
 fi
 if want ctrace; then
   cd /tmp && export TMPDIR=/tmp
-  for spec in "1 0 1" "0 16 2" "0 0 2"; do
-    set -- $spec
+  for spec in ${CTRACE_SPECS:-"1 0 1" "0 16 2" "0 0 2"}; do
+    set -- $(echo $spec | tr ',' ' ')
     rm -rf "$OUT/ctrace_$1_$2_$3"
-    RT_COPY_MODE=$1 RT_COPY_BLOCKS=$2 DEPTH=$3 timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv \
+    RT_COPY_KERNEL=${4:--1} RT_COPY_MODE=$1 RT_COPY_BLOCKS=$2 DEPTH=$3 timeout -k 10 120 rocprofv3 --kernel-trace \
+        --memory-copy-trace --output-format csv \
         -d "$OUT/ctrace_$1_$2_$3" -o run -- python3 "$GRAFT_REPO_ROOT/tools/copy_trace.py" > "$OUT/ctrace_$1_$2_$3.json" \
         2> "$OUT/ctrace_$1_$2_$3.err" || { echo "ctrace $spec failed"; tail -5 "$OUT/ctrace_$1_$2_$3.err"; exit 7; }
     cat "$OUT/ctrace_$1_$2_$3.json"; python3 "$GRAFT_REPO_ROOT/tools/copy_trace.py" parse "$OUT/ctrace_$1_$2_$3"
