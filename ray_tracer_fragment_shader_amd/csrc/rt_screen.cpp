@@ -26,7 +26,6 @@
 #include <cstdlib>
 #include <cstdint>
 #include <cstring>
-#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -53,12 +52,15 @@ inline V3 normalize(V3 a) {                                                     
     return v3(a.x / l, a.y / l, a.z / l);
 }
 
-// rand(): glibc's TYPE_3 additive feedback generator (RAND_MAX 2^31 - 1) or the MSVC CRT LCG (32767).
+// rand(): glibc's TYPE_3 additive feedback generator (RAND_MAX 2^31 - 1) or the MSVC CRT LCG (32767), produced
+// in blocks: the glibc state is the last 34 outputs of r[n] = r[n - 31] + r[n - 3] (mod 2^32), result r[n] >> 1.
 struct Rand {
+    static constexpr int kHist = 34, kBlock = 4096;
     int kind;
     uint32_t lcg;
-    int32_t r[34];
-    int i = 0;
+    uint32_t h[kHist + kBlock];                                      // history, then the block's raw values
+    int32_t out[kBlock];
+    int pos = kBlock;                                                // next unread entry of out
     Rand(int k, uint32_t seed) : kind(k), lcg(seed) {
         if (kind == RT_RAND_GLIBC) {                                  // srandom_r, TYPE_3
             std::vector<int32_t> t(344);
@@ -69,34 +71,50 @@ struct Rand {
             }
             for (int q = 31; q < 34; ++q) t[q] = t[q - 31];
             for (int q = 34; q < 344; ++q) t[q] = (int32_t)((uint32_t)t[q - 31] + (uint32_t)t[q - 3]);
-            for (int q = 0; q < 34; ++q) r[q] = t[310 + q];
+            for (int q = 0; q < kHist; ++q) h[q] = (uint32_t)t[310 + q];
         }
     }
-    int next() {
+    void refill() {
         if (kind == RT_RAND_MSVC) {
-            lcg = lcg * 214013u + 2531011u;
-            return (int)((lcg >> 16) & 0x7fff);
+            for (int k = 0; k < kBlock; ++k) {
+                lcg = lcg * 214013u + 2531011u;
+                out[k] = (int32_t)((lcg >> 16) & 0x7fff);
+            }
+        } else {
+            for (int k = kHist; k < kHist + kBlock; ++k) h[k] = h[k - 31] + h[k - 3];
+            for (int k = 0; k < kBlock; ++k) out[k] = (int32_t)(h[kHist + k] >> 1);
+            std::memcpy(h, h + kBlock, sizeof(uint32_t) * kHist);
         }
-        int32_t v = (int32_t)((uint32_t)r[(i + 3) % 34] + (uint32_t)r[(i + 31) % 34]);
-        r[i] = v;
-        i = (i + 1) % 34;
-        return (int)((uint32_t)v >> 1);
+        pos = 0;
+    }
+    int next() {
+        if (pos == kBlock) refill();
+        return out[pos++];
     }
     double max() const { return kind == RT_RAND_MSVC ? 32767.0 : 2147483647.0; }
 };
 
-// The stream of randomUnit() results (:1148-1169), generated on demand and kept from the first sample
-// not yet consumed by a resolved pixel.
+// The stream of randomUnit() results (:1148-1169), generated ahead in batches into one flat array and kept
+// from the first sample not yet consumed by a resolved pixel.
 struct Jitter {
     Rand rng;
-    uint64_t base = 0;                     // sample index of q.front()
-    std::deque<V3> q;
-    std::deque<uint32_t> calls;            // rand() calls of each sample
+    uint64_t base = 0;                     // sample index of xyz[0]
+    std::vector<double> xyz;               // 3 per sample
+    std::vector<uint32_t> calls;           // rand() calls of each sample
+    size_t n = 0;                          // samples generated from base on (the arrays hold more room)
+    uint64_t cons = 0;                     // first sample not yet consumed
     uint64_t consumed_calls = 0;
     Jitter(int kind, uint32_t seed) : rng(kind, seed) {}
-    const V3& at(uint64_t s) {
-        while (base + q.size() <= s) {
-            const double den = rng.max() + 1.0;
+    // samples up to index s (exclusive) generated
+    void ensure(uint64_t s) {
+        if (base + n >= s) return;
+        const size_t want = (size_t)(s - base) + 2048;               // a batch ahead
+        if (calls.size() < want) {
+            xyz.resize(3 * (want + want / 2));
+            calls.resize(want + want / 2);
+        }
+        const double den = rng.max() + 1.0;
+        for (; n < want; ++n) {
             V3 v = v3(0.0, 0.0, 0.0);
             uint32_t c = 0;
             while (v.x == 0 && v.y == 0 && v.z == 0) {                // vec.isZero() (:1160, :173)
@@ -106,18 +124,25 @@ struct Jitter {
                 c += 3;
                 v = v3(x, y, z);
             }
-            q.push_back(normalize(v));                               // vec.normalize() (:1166)
-            calls.push_back(c);
+            const V3 u = normalize(v);                               // vec.normalize() (:1166)
+            xyz[3 * n] = u.x, xyz[3 * n + 1] = u.y, xyz[3 * n + 2] = u.z;
+            calls[n] = c;
         }
-        return q[s - base];
     }
-    void consume_until(uint64_t s) {       // samples [base, s) now belong to resolved pixels
-        while (base < s) {
-            at(base);
-            consumed_calls += calls.front();
-            q.pop_front();
-            calls.pop_front();
-            ++base;
+    const double* at(uint64_t s) {         // the sample's x, y, z (valid until the next ensure / consume)
+        ensure(s + 1);
+        return &xyz[3 * (size_t)(s - base)];
+    }
+    void consume_until(uint64_t s) {       // samples [cons, s) now belong to resolved pixels
+        ensure(s);
+        for (uint64_t q = cons; q < s; ++q) consumed_calls += calls[(size_t)(q - base)];
+        cons = std::max(cons, s);
+        const size_t k = (size_t)(cons - base);
+        if (k > 4096 && k > n / 2) {       // drop the consumed front (amortised)
+            std::memmove(xyz.data(), xyz.data() + 3 * k, sizeof(double) * 3 * (n - k));
+            std::memmove(calls.data(), calls.data() + k, sizeof(uint32_t) * (n - k));
+            base += k;
+            n -= k;
         }
     }
 };
@@ -348,10 +373,8 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         c.spred_end = spred;
         c.jend = c.S0 + (uint64_t)jmax;
         c.walk_end = w;
-        for (int k = 0; k < jmax; ++k) {                             // randomUnit() values S0 .. S0 + jmax - 1
-            const V3& v = jit.at(c.S0 + (uint64_t)k);
-            hj[3 * k] = v.x, hj[3 * k + 1] = v.y, hj[3 * k + 2] = v.z;
-        }
+        if (jmax > 0)                                                // randomUnit() values S0 .. S0 + jmax - 1
+            std::memcpy(hj, jit.at(c.S0 + (uint64_t)(jmax - 1)) - 3 * (size_t)(jmax - 1), sizeof(double) * 3 * jmax);
         // One round trip: form the rays, trace them (colours straight into host memory).
         int r = rt_screen_form_ends(static_cast<const ScreenPix*>(B.d_pix), m, static_cast<const double*>(B.d_jit),
                                     static_cast<double*>(B.d_end.p), st.s);
@@ -381,7 +404,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         }
         // While the GPU traces: generate the stream values the following chunk will need (rand() + normalize
         // are the host's largest share of a round trip), so its build only copies them.
-        (void)jit.at(have_next ? nxt.jend + (nxt.jend - nxt.S0) + 64 : cur.jend + 64);
+        jit.ensure(have_next ? nxt.jend + (nxt.jend - nxt.S0) + 64 : cur.jend + 64);
         const auto c1 = clk::now();
         e = hipEventSynchronize(buf[cur.b].done);
         if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(e));
