@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "../../include/rt_api.h"
+#include "rt_layout.hpp"
 
 // Record `msg` as this thread's rt_last_error() and return `code`.
 int rt_fail(int code, const std::string& msg);
@@ -39,20 +40,15 @@ int rt_unshuffle_dev_ex(const void* gathered, const void* rank0_slab, void* imag
 int rt_unpack_dev_ex(const void* gathered, const void* rank0_slab, void* image, int W, int H, int src_format,
                      int dst_format, int band_height, int n_ranks, int slab_rows, void* stream);
 
-// rt_render_screen's device-side ray formation (rt_kernel.hip).  One pixel of a chunk: its screen point and
-// the window of jitter-stream samples traced for it (stream indices base .. base + len - 1, relative to the
-// chunk's first stream index), whose rays occupy ends[off .. off + len - 1].
-struct ScreenPix {
-    double sp[3];
-    int32_t base, len, off, pad;
-};
-constexpr int kScreenMaxWindow = 128;          // len <= this (one workgroup per pixel)
+// rt_render_screen's chunk traced in one launch (rt_kernel.hip): ray k of the chunk, window entry j of pixel q
+// (pix[q].off <= k < pix[q].off + pix[q].len), is Line(cam, pix[q].sp + 0.5 * jit[pix[q].base + j])
+// (ray.set(camera, screenPt + .5 * randomUnit()), MSA:1296); first[b] = the pixel of ray b * kScreenBlock.
+// All pointers device-visible; n rays, m pixels.
+int rt_trace_screen_dev(rt_ctx* c, const double cam[3], const ScreenPix* pix, const int32_t* first, int m,
+                        const double* jit, int n, int depth, double* rgb64f, void* stream);
 constexpr int kScreenMaxRays = 1 << 19;        // rays of one chunk
 constexpr int kScreenMaxPix = 4096;            // pixels of one chunk
 constexpr int kScreenMaxJit = kScreenMaxPix * 16 + 128;   // stream values of one chunk
+constexpr int kScreenMaxBlocks = (kScreenMaxRays + kScreenBlock - 1) / kScreenBlock;
 // Frees the rt_render_screen buffers kept for `ctx` (rt_ctx_destroy).
 void rt_screen_release(const rt_ctx* ctx);
-// ends[off + j] = sp + 0.5 * jit[base + j] for every pixel of `pix` (device-visible), j < len (MSA:1296).
-int rt_screen_form_ends(const ScreenPix* pix, int m, const double* jit, double* ends, void* stream);
-// out[k] = p for k < n (the rays' common start, the camera).
-int rt_fill_points(double* out, int n, const double p[3], void* stream);

@@ -1115,29 +1115,43 @@ extern "C" int rt_host_free(void* p) {
     return RT_OK;
 }
 
+static int trace_rays_launch(rt_ctx* c, const double* starts, const double* ends, int n, int depth, double* rgb64f,
+                             uint32_t* raycount, hipStream_t st, const ScreenArgs& sa) {
+    RT_HIP(hipSetDevice(c->device));
+    const dim3 grid((unsigned)((n + kThreads - 1) / kThreads));
+    const int v = c->tree ? 2 : c->transparent ? 1 : 0;
+    hipError_t e;
+    switch (depth) {
+        case 0: e = launch_trace_rays<0>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount, sa); break;
+        case 1: e = launch_trace_rays<1>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount, sa); break;
+        case 2: e = launch_trace_rays<2>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount, sa); break;
+        case 3: e = launch_trace_rays<3>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount, sa); break;
+        case 4: e = launch_trace_rays<4>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount, sa); break;
+        case 5: e = launch_trace_rays<5>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount, sa); break;
+        case 6: e = launch_trace_rays<6>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount, sa); break;
+        default: e = launch_trace_rays<7>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount, sa); break;
+    }
+    if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_trace_rays_kernel: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
 extern "C" int rt_trace_rays_dev(rt_ctx* c, const double* starts, const double* ends, int n, int depth,
                                  double* rgb64f, uint32_t* raycount, void* stream) {
     if (!c || !c->scene_set) return rt_fail(RT_EINVAL, "rt_trace_rays_dev: no context/scene");
     if (n < 0 || (n > 0 && (!starts || !ends))) return rt_fail(RT_EINVAL, "rt_trace_rays_dev: bad rays");
     if (depth < 0 || depth > RT_MAX_DEPTH) return rt_fail(RT_EINVAL, "rt_trace_rays_dev: depth out of range");
     if (n == 0) return RT_OK;
-    RT_HIP(hipSetDevice(c->device));
-    const dim3 grid((unsigned)((n + kThreads - 1) / kThreads));
-    const int v = c->tree ? 2 : c->transparent ? 1 : 0;
-    const hipStream_t st = (hipStream_t)stream;
-    hipError_t e;
-    switch (depth) {
-        case 0: e = launch_trace_rays<0>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
-        case 1: e = launch_trace_rays<1>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
-        case 2: e = launch_trace_rays<2>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
-        case 3: e = launch_trace_rays<3>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
-        case 4: e = launch_trace_rays<4>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
-        case 5: e = launch_trace_rays<5>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
-        case 6: e = launch_trace_rays<6>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
-        default: e = launch_trace_rays<7>(v, grid, st, c->d_scene, starts, ends, n, rgb64f, raycount); break;
-    }
-    if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_trace_rays_kernel: ") + hipGetErrorString(e));
-    return RT_OK;
+    return trace_rays_launch(c, starts, ends, n, depth, rgb64f, raycount, (hipStream_t)stream, ScreenArgs{});
+}
+
+int rt_trace_screen_dev(rt_ctx* c, const double cam[3], const ScreenPix* pix, const int32_t* first, int m,
+                        const double* jit, int n, int depth, double* rgb64f, void* stream) {
+    if (!c || !c->scene_set) return rt_fail(RT_EINVAL, "rt_trace_screen_dev: no context/scene");
+    if (depth < 0 || depth > RT_MAX_DEPTH) return rt_fail(RT_EINVAL, "rt_trace_screen_dev: depth out of range");
+    if (n <= 0 || m <= 0) return RT_OK;
+    ScreenArgs sa;
+    sa.pix = pix, sa.m = m, sa.first = first, sa.jit = jit;
+    return trace_rays_launch(c, cam, nullptr, n, depth, rgb64f, nullptr, (hipStream_t)stream, sa);
 }
 
 extern "C" int rt_intersect_dev(rt_ctx* c, const double* starts, const double* ends, int n, rt_hit* hits,
@@ -1281,46 +1295,6 @@ extern "C" int rt_diag_kernel_occupancy(int depth, int variant, int lds_bytes, i
     }
     if (!f) return rt_fail(RT_EINVAL, "rt_diag_kernel_occupancy: kernel not built");
     RT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, RT_WG_FAST, (size_t)lds_bytes));
-    return RT_OK;
-}
-
-// rt_render_screen's jittered rays, formed on the device: ray j of pixel q ends at sp_q + 0.5 * jitter[base_q + j]
-// (ray.set(camera, screenPt + .5 * randomUnit()), MSA:1296; 0.5 * x is exact and the sum rounds as the host's).
-__global__ __launch_bounds__(kScreenMaxWindow) void rt_screen_ends_kernel(const ScreenPix* __restrict__ pix,
-                                                                         const double* __restrict__ jit,
-                                                                         double* __restrict__ ends) {
-    const ScreenPix& P = pix[blockIdx.x];
-    const int j = threadIdx.x;
-    if (j >= P.len) return;
-    const double* J = jit + 3 * (size_t)(P.base + j);
-    double* e = ends + 3 * (size_t)(P.off + j);
-    e[0] = P.sp[0] + 0.5 * J[0];
-    e[1] = P.sp[1] + 0.5 * J[1];
-    e[2] = P.sp[2] + 0.5 * J[2];
-}
-
-__global__ __launch_bounds__(256) void rt_fill_points_kernel(double* __restrict__ out, int n, double x, double y,
-                                                             double z) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= n) return;
-    out[3 * k] = x;
-    out[3 * k + 1] = y;
-    out[3 * k + 2] = z;
-}
-
-int rt_screen_form_ends(const ScreenPix* pix, int m, const double* jit, double* ends, void* stream) {
-    if (m <= 0) return RT_OK;
-    hipLaunchKernelGGL(rt_screen_ends_kernel, dim3((unsigned)m), dim3(kScreenMaxWindow), 0, (hipStream_t)stream, pix,
-                       jit, ends);
-    RT_HIP(hipGetLastError());
-    return RT_OK;
-}
-
-int rt_fill_points(double* out, int n, const double p[3], void* stream) {
-    if (n <= 0) return RT_OK;
-    hipLaunchKernelGGL(rt_fill_points_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       out, n, p[0], p[1], p[2]);
-    RT_HIP(hipGetLastError());
     return RT_OK;
 }
 

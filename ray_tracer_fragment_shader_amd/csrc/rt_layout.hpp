@@ -159,3 +159,13 @@ inline constexpr int scene_bytes_for(int n, int n_meshes = 0, int n_tris = 0, in
 }
 
 }  // namespace rt
+
+// rt_render_screen's chunk (rt_screen.cpp), read by the screen mode of rt_trace_rays_kernel: one pixel's screen point
+// and the window of jitter-stream samples traced for it (stream indices base .. base + len - 1, relative to the
+// chunk's first stream index), whose rays are ray indices off .. off + len - 1 of the launch.
+struct ScreenPix {
+    double sp[3];
+    int32_t base, len, off, pad;
+};
+constexpr int kScreenMaxWindow = 128;          // len <= this
+constexpr int kScreenBlock = 256;              // rays per first-pixel table entry (the trace kernel's workgroup)

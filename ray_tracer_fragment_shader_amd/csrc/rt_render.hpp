@@ -427,30 +427,55 @@ void rt_render_kernel_sg(const DevScene* __restrict__ gscene, RenderParams P, vo
 
 // rayTraceRay on a list of rays Line(starts[k], ends[k]).  Rays from arbitrary starts: whether their hit
 // points may skip the bounding-sphere cull is decided per ray (hits_ok_from).
+// Screen mode (spix != nullptr, rt_render_screen's chunks): every ray starts at starts[0..2] (the camera) and ends at
+// its pixel's screen point + 0.5 * its jitter value (MSA:1296), formed here instead of by a launch of its own.
 template <int B, bool TRANSP, bool TREE = false>
 __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene* __restrict__ S,
                                                                  const double* __restrict__ starts,
                                                                  const double* __restrict__ ends, int n,
                                                                  double* __restrict__ rgb,
-                                                                 uint32_t* __restrict__ rc) {
+                                                                 uint32_t* __restrict__ rc,
+                                                                 const ScreenPix* __restrict__ spix, int sm,
+                                                                 const int32_t* __restrict__ sfirst,
+                                                                 const double* __restrict__ sjit) {
+    static_assert(kThreads == kScreenBlock, "one first-pixel entry per workgroup");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // Every lane traces (trace() reduces over the wave); lanes past n repeat ray n - 1 and store nothing.
     const int k = blockIdx.x * kThreads + threadIdx.x, kk = k < n ? k : n - 1;
     uint32_t seg = 0, sh = 0;
     SceneView V = view_of(S, S, S->n_padded, S->n_stride, S->n_lights);
-    const d3 p0 = ld3(starts + 3 * kk);
+    d3 p0, p1;
+    if (spix) {
+        p0 = ld3(starts);
+        int q = sfirst[blockIdx.x];                         // the pixel of the workgroup's first ray
+        while (q + 1 < sm && spix[q + 1].off <= kk) ++q;
+        const ScreenPix& X = spix[q];
+        const double* J = sjit + 3 * (size_t)(X.base + (kk - X.off));
+        p1 = d3{X.sp[0] + 0.5 * J[0], X.sp[1] + 0.5 * J[1], X.sp[2] + 0.5 * J[2]};
+    } else {
+        p0 = ld3(starts + 3 * kk);
+        p1 = ld3(ends + 3 * kk);
+    }
     V.hits_ok = hits_ok_from(S, p0);
     double* slot = reinterpret_cast<double*>(smem) + threadIdx.x;
     int* mslot = reinterpret_cast<int*>(smem + 3 * 8 * colour_slots(B, TRANSP) * kSlotStride) + threadIdx.x;
     d3 c;
     if constexpr (TREE)
-        c = trace_tree<B>(V, p0, ld3(ends + 3 * kk), &seg, &sh);
+        c = trace_tree<B>(V, p0, p1, &seg, &sh);
     else
-        c = trace<B, false, TRANSP, false>(V, p0, ld3(ends + 3 * kk), ~0ull, &seg, &sh, slot, mslot);
+        c = trace<B, false, TRANSP, false>(V, p0, p1, ~0ull, &seg, &sh, slot, mslot);
     if (k >= n) return;
     if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
     if (rc) rc[k] = seg | (sh << 16);
 }
+
+// The screen-mode arguments of a trace launch (all null: a plain ray list).
+struct ScreenArgs {
+    const ScreenPix* pix = nullptr;
+    int m = 0;
+    const int32_t* first = nullptr;
+    const double* jit = nullptr;
+};
 
 // Render-kernel variants rt_render_dev chooses between (rt_kernel.hip).
 enum RenderVariant {
@@ -489,7 +514,8 @@ template <int B>
 hipError_t launch_render(const RenderLaunch& L);
 template <int B>
 hipError_t launch_trace_rays(int variant /* 0 opaque, 1 FULL, 2 tree */, dim3 grid, hipStream_t st,
-                             const DevScene* s, const double* a, const double* b, int n, double* rgb, uint32_t* rc);
+                             const DevScene* s, const double* a, const double* b, int n, double* rgb, uint32_t* rc,
+                             const ScreenArgs& sa);
 template <int B>
 const void* render_kernel_ptr(int variant);   // rt_diag_kernel_resources: 0 fast, 1 cull, 2 FULL, 3 tree
 
@@ -498,7 +524,7 @@ const void* render_kernel_ptr(int variant);   // rt_diag_kernel_resources: 0 fas
     hipError_t launch_render<B>(const RenderLaunch& L);                                                        \
     template <>                                                                                                \
     hipError_t launch_trace_rays<B>(int, dim3, hipStream_t, const DevScene*, const double*, const double*, int,   \
-                                    double*, uint32_t*);                                                       \
+                                    double*, uint32_t*, const ScreenArgs&);                                    \
     template <>                                                                                                \
     const void* render_kernel_ptr<B>(int);
 RT_DECLARE_DEPTH(0) RT_DECLARE_DEPTH(1) RT_DECLARE_DEPTH(2) RT_DECLARE_DEPTH(3)
@@ -562,18 +588,19 @@ hipError_t launch_render_impl(const RenderLaunch& L) {
 
 template <int B>
 hipError_t launch_trace_rays_impl(int variant, dim3 grid, hipStream_t st, const DevScene* s, const double* a,
-                                  const double* b, int n, double* rgb, uint32_t* rc) {
+                                  const double* b, int n, double* rgb, uint32_t* rc, const ScreenArgs& sa) {
     if constexpr (B > RT_MAX_B) {
         return hipErrorInvalidValue;
     } else {
         if (variant == 2)
-            hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, true>), grid, dim3(kThreads), 0, st, s, a, b, n, rgb, rc);
+            hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, true>), grid, dim3(kThreads), 0, st, s, a, b, n, rgb, rc,
+                               sa.pix, sa.m, sa.first, sa.jit);
         else if (variant == 1)
             hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, false>), grid, dim3(kThreads), slot_bytes(B, true), st, s,
-                               a, b, n, rgb, rc);
+                               a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit);
         else
             hipLaunchKernelGGL((rt_trace_rays_kernel<B, false, false>), grid, dim3(kThreads), slot_bytes(B, false), st,
-                               s, a, b, n, rgb, rc);
+                               s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit);
         return hipGetLastError();
     }
 }
@@ -606,8 +633,8 @@ const void* render_kernel_ptr_impl(int variant) {
     hipError_t launch_render<B>(const RenderLaunch& L) { return launch_render_impl<B>(L); }                    \
     template <>                                                                                                \
     hipError_t launch_trace_rays<B>(int v, dim3 g, hipStream_t st, const DevScene* s, const double* a,         \
-                                    const double* b, int n, double* rgb, uint32_t* rc) {                       \
-        return launch_trace_rays_impl<B>(v, g, st, s, a, b, n, rgb, rc);                                       \
+                                    const double* b, int n, double* rgb, uint32_t* rc, const ScreenArgs& sa) { \
+        return launch_trace_rays_impl<B>(v, g, st, s, a, b, n, rgb, rc, sa);                                   \
     }                                                                                                          \
     template <>                                                                                                \
     const void* render_kernel_ptr<B>(int v) { return render_kernel_ptr_impl<B>(v); }                           \

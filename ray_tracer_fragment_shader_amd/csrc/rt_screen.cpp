@@ -152,12 +152,6 @@ inline unsigned char to_u8(double c) {
     return (unsigned char)(int)std::floor(v * 255.0 + 0.5);
 }
 
-struct DevBuf {
-    void* p = nullptr;
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-};
 struct HostBuf {
     void* p = nullptr;
     ~HostBuf() {
@@ -171,8 +165,7 @@ struct Stream {
     }
 };
 
-struct ScreenBuf {                                                    // one chunk's device / mapped buffers
-    DevBuf d_end;
+struct ScreenBuf {                                                    // one chunk's mapped buffers
     HostBuf h_rgb, h_pix, h_jit;
     void* d_rgb = nullptr;
     void* d_pix = nullptr;
@@ -184,20 +177,24 @@ struct ScreenBuf {                                                    // one chu
 };
 struct ScreenWs {                                                    // two chunks in flight + the rays' start
     Stream st;
-    DevBuf d_start;
+    HostBuf h_cam;
+    void* d_cam = nullptr;
     ScreenBuf buf[2];
 };
+// A chunk's pixel table, then its first-pixel table (one entry per kScreenBlock rays).
+constexpr size_t kPixBytes = (size_t)kScreenMaxPix * sizeof(ScreenPix);
+constexpr size_t kPixTableBytes = kPixBytes + (size_t)kScreenMaxBlocks * sizeof(int32_t);
 
 std::unique_ptr<ScreenWs> alloc_ws() {
     std::unique_ptr<ScreenWs> w(new ScreenWs());
     const size_t ray_bytes = (size_t)kScreenMaxRays * 3 * sizeof(double);
     const unsigned mapped = hipHostMallocMapped | hipHostMallocCoherent;
     hipError_t e = hipStreamCreateWithFlags(&w->st.s, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(&w->d_start.p, ray_bytes);
+    if (e == hipSuccess) e = hipHostMalloc(&w->h_cam.p, 3 * sizeof(double), mapped);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&w->d_cam, w->h_cam.p, 0);
     for (ScreenBuf& b : w->buf) {
-        if (e == hipSuccess) e = hipMalloc(&b.d_end.p, ray_bytes);
         if (e == hipSuccess) e = hipHostMalloc(&b.h_rgb.p, ray_bytes, mapped);
-        if (e == hipSuccess) e = hipHostMalloc(&b.h_pix.p, (size_t)kScreenMaxPix * sizeof(ScreenPix), mapped);
+        if (e == hipSuccess) e = hipHostMalloc(&b.h_pix.p, kPixTableBytes, mapped);
         if (e == hipSuccess) e = hipHostMalloc(&b.h_jit.p, (size_t)kScreenMaxJit * 3 * sizeof(double), mapped);
         if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_rgb, b.h_rgb.p, 0);
         if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_pix, b.h_pix.p, 0);
@@ -269,8 +266,8 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // pixel, the samples of a window of kWin stream indices either side of its predicted range, so the chunk
     // keeps resolving while the actual stream position drifts by up to kWin from the prediction (a count that
     // differs at an object edge no longer ends the chunk).  The jittered rays are formed on the device from the
-    // chunk's randomUnit() values (rt_screen_form_ends): the host generates each stream value once and sends
-    // 24 bytes per value instead of the rays.  Simulated on the reference's own sample counts (demo frame):
+    // chunk's randomUnit() values by the trace launch itself (rt_trace_screen_dev): the host generates each stream
+    // value once and sends 24 bytes per value instead of the rays, and a chunk is one launch.  Simulated on the reference's own sample counts (demo frame):
     // 759 round trips instead of 2,515, for ~85 traced samples per pixel instead of 7.
     //
     // Two chunks in flight (r04).  While the GPU traces chunk c, the host builds and queues chunk c + 1 as the
@@ -282,7 +279,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // samples at its actual stream position, or breaks.
     const int kMaxRays = kScreenMaxRays, kMaxPix = kScreenMaxPix, kWin = 28;
     const int kMaxJit = kScreenMaxJit;
-    static_assert(16 + 2 * kWin <= kScreenMaxWindow, "window exceeds the ray-formation workgroup");
+    static_assert(16 + 2 * kWin <= kScreenMaxWindow, "window longer than a pixel table entry allows");
     static_assert(kScreenMaxJit >= kScreenMaxPix * 16 + 2 * kWin + 16, "stream-value buffer too small");
     // The buffers live in the context between calls (allocating ~40 MB of device and mapped host memory
     // per frame cost more than a quarter of a demo frame); a call running concurrently on the same context
@@ -297,13 +294,11 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
             give_ws(ctx, std::move(ws));
         }
     } give{ctx, ws};
-    DevBuf& d_start = ws->d_start;
     ScreenBuf* buf = ws->buf;
     Stream& st = ws->st;
     hipError_t e = hipSuccess;
-    const double cam_p[3] = {camera.x, camera.y, camera.z};
-    rc = rt_fill_points(static_cast<double*>(d_start.p), kMaxRays, cam_p, st.s);
-    if (rc) return rc;
+    double* hc = static_cast<double*>(ws->h_cam.p);                  // the rays' start: the camera
+    hc[0] = camera.x, hc[1] = camera.y, hc[2] = camera.z;
 
     Jitter jit(rand_kind, seed);
     V3 avgColor = v3(0.0, 0.0, 0.0);                                 // :1283, carried across pixels
@@ -340,6 +335,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         const auto c0 = clk::now();
         ScreenBuf& B = buf[b];
         ScreenPix* hp = static_cast<ScreenPix*>(B.h_pix.p);
+        int32_t* hf = reinterpret_cast<int32_t*>(static_cast<char*>(B.h_pix.p) + kPixBytes);
         double* hj = static_cast<double*>(B.h_jit.p);
         c.b = b;
         c.p0 = p0;
@@ -347,7 +343,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         c.sp.resize(kMaxPix);
         int m = (int)std::min<long long>(want, P - p0);
         V3 w = w0;
-        int total = 0, jmax = 0;
+        int total = 0, jmax = 0, nb = 0;
         long long spred = (long long)pred_start - (long long)c.S0;  // predicted first sample, relative to S0
         for (int q = 0; q < m; ++q) {
             const long long pix = p0 + q;
@@ -363,6 +359,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
             c.sp[q] = w;
             hp[q].sp[0] = w.x, hp[q].sp[1] = w.y, hp[q].sp[2] = w.z;
             hp[q].base = (int32_t)lo, hp[q].len = len, hp[q].off = total, hp[q].pad = 0;
+            for (; nb * kScreenBlock < total + len; ++nb) hf[nb] = q;  // workgroups whose first ray is q's
             total += len;
             jmax = std::max(jmax, (int)hi);
             spred += pred;
@@ -375,11 +372,12 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         c.walk_end = w;
         if (jmax > 0)                                                // randomUnit() values S0 .. S0 + jmax - 1
             std::memcpy(hj, jit.at(c.S0 + (uint64_t)(jmax - 1)) - 3 * (size_t)(jmax - 1), sizeof(double) * 3 * jmax);
-        // One round trip: form the rays, trace them (colours straight into host memory).
-        int r = rt_screen_form_ends(static_cast<const ScreenPix*>(B.d_pix), m, static_cast<const double*>(B.d_jit),
-                                    static_cast<double*>(B.d_end.p), st.s);
-        if (!r) r = rt_trace_rays_dev(ctx, static_cast<const double*>(d_start.p), static_cast<const double*>(B.d_end.p),
-                                      total, depth, static_cast<double*>(B.d_rgb), nullptr, st.s);
+        // One round trip: one launch forms the rays and traces them (colours straight into host memory).
+        const int r = rt_trace_screen_dev(ctx, static_cast<const double*>(ws->d_cam),
+                                          static_cast<const ScreenPix*>(B.d_pix),
+                                          reinterpret_cast<const int32_t*>(static_cast<const char*>(B.d_pix) + kPixBytes),
+                                          m, static_cast<const double*>(B.d_jit), total, depth,
+                                          static_cast<double*>(B.d_rgb), st.s);
         if (r) return r;
         const hipError_t er = hipEventRecord(B.done, st.s);
         if (er != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(er));

@@ -100,21 +100,24 @@ extern "C" int rt_trace_rays_dev(rt_ctx* c, const double* starts, const double* 
     return oracle_trace_rays(&c->scene, starts, ends, n, depth, rgb64f, raycount, 1);
 }
 // rt_render_screen's device-side ray formation (rt_kernel.hip), restated on the host with the same operations.
-int rt_screen_form_ends(const ScreenPix* pix, int m, const double* jit, double* ends, void*) {
-    for (int q = 0; q < m; ++q) {
+int rt_trace_screen_dev(rt_ctx* c, const double cam[3], const ScreenPix* pix, const int32_t* first, int m,
+                        const double* jit, int n, int depth, double* rgb64f, void*) {
+    if (!c) return rt_fail(RT_EINVAL, "rt_trace_screen_dev: null context");
+    if (n <= 0 || m <= 0) return RT_OK;
+    std::vector<double> starts(3 * (size_t)n), ends(3 * (size_t)n);
+    for (int k = 0; k < n; ++k) {                             // the device's pixel lookup, from the first-pixel table
+        int q = first[k / kScreenBlock];
+        if (q < 0 || q >= m || pix[q].off > (k / kScreenBlock) * kScreenBlock)
+            return rt_fail(RT_EINVAL, "rt_trace_screen_dev: bad first-pixel table");
+        while (q + 1 < m && pix[q + 1].off <= k) ++q;
         const ScreenPix& P = pix[q];
-        if (P.len < 0 || P.len > kScreenMaxWindow) return rt_fail(RT_EINVAL, "rt_screen_form_ends: bad window");
-        for (int j = 0; j < P.len; ++j) {
-            const double* J = jit + 3 * (size_t)(P.base + j);
-            double* e = ends + 3 * (size_t)(P.off + j);
-            e[0] = P.sp[0] + 0.5 * J[0];
-            e[1] = P.sp[1] + 0.5 * J[1];
-            e[2] = P.sp[2] + 0.5 * J[2];
+        if (P.len < 1 || P.len > kScreenMaxWindow || k >= P.off + P.len)
+            return rt_fail(RT_EINVAL, "rt_trace_screen_dev: ray outside its pixel's window");
+        const double* J = jit + 3 * (size_t)(P.base + (k - P.off));
+        for (int d = 0; d < 3; ++d) {
+            starts[3 * (size_t)k + d] = cam[d];
+            ends[3 * (size_t)k + d] = P.sp[d] + 0.5 * J[d];
         }
     }
-    return RT_OK;
-}
-int rt_fill_points(double* out, int n, const double p[3], void*) {
-    for (int k = 0; k < n; ++k) out[3 * k] = p[0], out[3 * k + 1] = p[1], out[3 * k + 2] = p[2];
-    return RT_OK;
+    return oracle_trace_rays(&c->scene, starts.data(), ends.data(), n, depth, rgb64f, nullptr, 1);
 }
