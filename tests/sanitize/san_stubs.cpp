@@ -119,5 +119,6 @@ int rt_trace_screen_dev(rt_ctx* c, const double cam[3], const ScreenPix* pix, co
             ends[3 * (size_t)k + d] = P.sp[d] + 0.5 * J[d];
         }
     }
-    return oracle_trace_rays(&c->scene, starts.data(), ends.data(), n, depth, rgb64f, nullptr, 1);
+    const char* th = getenv("SAN_TRACE_THREADS");
+    return oracle_trace_rays(&c->scene, starts.data(), ends.data(), n, depth, rgb64f, nullptr, th ? atoi(th) : 1);
 }

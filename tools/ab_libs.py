@@ -5,6 +5,8 @@ their renders interleaved round by round — so box-to-box and process-to-proces
 cancel out.
 
 usage: ab_libs.py [c2,c3,c5] [rounds]        prints one JSON line per (config, lib): median / min kernel ms
+INFLIGHT=k: bench.py's timed pattern instead — k contexts, streams and output buffers per build, frames issued
+round-robin, per-frame interval = (last stream's end - start) / frames.
 """
 import ctypes
 import glob
@@ -48,16 +50,29 @@ def main():
         if only is None or name in only:
             libs[name] = load(d, tmp, name)
     st = torch.cuda.current_stream()
+    nfly = int(os.environ.get("INFLIGHT", "0"))
     ctxs, bufs = {}, {}
     for name, L in libs.items():
         c = ctypes.c_void_p()
         abi.check(L.rt_ctx_create(0, ctypes.byref(c)), "rt_ctx_create")
         ctxs[name] = c
+    fly_ctx = {}
+    sts = [torch.cuda.Stream() for _ in range(nfly)]
+    for name, L in libs.items():
+        fly_ctx[name] = []
+        for _ in range(nfly):
+            c = ctypes.c_void_p()
+            abi.check(L.rt_ctx_create(0, ctypes.byref(c)), "rt_ctx_create")
+            fly_ctx[name].append(c)
     res = {(c, n): [] for c in cfgs for n in libs}
+    fly_bufs = {}
     for c in cfgs:
         cfg = scenes.CONFIGS[c]
         bufs[c] = (torch.empty((cfg.height, cfg.width, 4), dtype=torch.float32, device="cuda"),
                    torch.empty((cfg.height, cfg.width, 4), dtype=torch.uint8, device="cuda"))
+        fly_bufs[c] = [(torch.empty((cfg.height, cfg.width, 4), dtype=torch.float32, device="cuda"),
+                        torch.empty((cfg.height, cfg.width, 4), dtype=torch.uint8, device="cuda"))
+                       for _ in range(nfly)]
     for r in range(rounds + 1):                       # round 0: untimed warm-up / calibration / clock settle
         for c in cfgs:
             cfg = scenes.CONFIGS[c]
@@ -72,6 +87,30 @@ def main():
                     cams.append(cm)
             b32, b8 = bufs[c]
             for name, L in libs.items():
+                if nfly:
+                    fl = []
+                    for j in range(nfly):
+                        abi.check(L.rt_set_scene(fly_ctx[name][j], ctypes.byref(sa)), "rt_set_scene")
+                        fl.append((fly_ctx[name][j], ctypes.byref(cams[0]), cfg.width, cfg.height, cfg.depth, None,
+                                   ctypes.c_void_p(fly_bufs[c][j][0].data_ptr()),
+                                   ctypes.c_void_p(fly_bufs[c][j][1].data_ptr()), None, None,
+                                   ctypes.c_void_p(sts[j].cuda_stream)))
+                    for i in range(3 * nfly if r else 40):
+                        abi.check(L.rt_render_dev(*fl[i % nfly]), "rt_render_dev")
+                    torch.cuda.synchronize()
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record(sts[0])
+                    for i in range(reps):
+                        L.rt_render_dev(*fl[i % nfly])
+                    ends = []
+                    for j in range(nfly):
+                        e = torch.cuda.Event(enable_timing=True)
+                        e.record(sts[j])
+                        ends.append(e)
+                    torch.cuda.synchronize()
+                    if r:
+                        res[(c, name)].append(max(e0.elapsed_time(e) for e in ends) / reps)
+                    continue
                 abi.check(L.rt_set_scene(ctxs[name], ctypes.byref(sa)), "rt_set_scene")
                 las = [(ctxs[name], ctypes.byref(cam), cfg.width, cfg.height, cfg.depth, None,
                         ctypes.c_void_p(b32.data_ptr()), ctypes.c_void_p(b8.data_ptr()), None, None,
@@ -111,6 +150,8 @@ def main():
                           "vs_base": round(med / base - 1, 4)}))
     for name, L in libs.items():
         L.rt_ctx_destroy(ctxs[name])
+        for c in fly_ctx[name]:
+            L.rt_ctx_destroy(c)
 
 
 if __name__ == "__main__":
