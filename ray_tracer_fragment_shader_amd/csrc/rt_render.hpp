@@ -37,7 +37,7 @@
 #define RT_MINW 0
 #endif
 #ifndef RT_NT_STORES
-#define RT_NT_STORES 0                         // 1: non-temporal RGBA32F/RGBA8 stores (A/B)
+#define RT_NT_STORES 1                         // non-temporal RGBA32F/RGBA8 stores (0: A/B)
 #endif
 #ifndef RT_WG_FAST
 #define RT_WG_FAST 64                          // workgroup of the default render kernels: 64 (8 x 8) or 128 (16 x 8)

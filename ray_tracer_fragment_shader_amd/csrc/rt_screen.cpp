@@ -113,20 +113,32 @@ struct Jitter {
             xyz.resize(3 * (want + want / 2));
             calls.resize(want + want / 2);
         }
-        const double den = rng.max() + 1.0;
-        for (; n < want; ++n) {
-            V3 v = v3(0.0, 0.0, 0.0);
-            uint32_t c = 0;
-            while (v.x == 0 && v.y == 0 && v.z == 0) {                // vec.isZero() (:1160, :173)
-                double z = (double)rng.next() / den - .5;            // Point(rand, rand, rand): the
-                double y = (double)rng.next() / den - .5;            // arguments are evaluated right to
-                double x = (double)rng.next() / den - .5;            // left (g++ and MSVC)
-                c += 3;
-                v = v3(x, y, z);
+        // rand() / (RAND_MAX + 1.0) divides by a power of two: the product with its reciprocal is the same double.
+        const double inv = 1.0 / (rng.max() + 1.0);
+        const int32_t half = (int32_t)((rng.max() + 1.0) / 2);       // the draw that makes a coordinate exactly 0
+        constexpr int kB = 512;
+        int32_t X[kB], Y[kB], Z[kB];
+        while (n < want) {
+            const int cnt = (int)std::min<size_t>(kB, want - n);
+            for (int k = 0; k < cnt; ++k) {                          // the draws (integer work, in order)
+                uint32_t c = 0;
+                int32_t z, y, x;
+                do {                                                 // vec.isZero() (:1160, :173): draw again
+                    z = rng.next();                                  // Point(rand, rand, rand): the arguments
+                    y = rng.next();                                  // are evaluated right to left (g++, MSVC)
+                    x = rng.next();
+                    c += 3;
+                } while (x == half && y == half && z == half);
+                X[k] = x, Y[k] = y, Z[k] = z;
+                calls[n + k] = c;
             }
-            const V3 u = normalize(v);                               // vec.normalize() (:1166)
-            xyz[3 * n] = u.x, xyz[3 * n + 1] = u.y, xyz[3 * n + 2] = u.z;
-            calls[n] = c;
+            double* o = &xyz[3 * n];
+            for (int k = 0; k < cnt; ++k) {                          // randomUnit(): (r / den - .5), normalize()
+                const double x = (double)X[k] * inv - .5, y = (double)Y[k] * inv - .5, z = (double)Z[k] * inv - .5;
+                const double l = std::sqrt(x * x + y * y + z * z);   // length() (:174)
+                o[3 * k] = x / l, o[3 * k + 1] = y / l, o[3 * k + 2] = z / l;   // (:175)
+            }
+            n += cnt;
         }
     }
     const double* at(uint64_t s) {         // the sample's x, y, z (valid until the next ensure / consume)
@@ -165,7 +177,8 @@ struct Stream {
     }
 };
 
-struct ScreenBuf {                                                    // one chunk's mapped buffers
+struct ScreenBuf {                                                    // one chunk's stream and mapped buffers
+    Stream st;
     HostBuf h_rgb, h_pix, h_jit;
     void* d_rgb = nullptr;
     void* d_pix = nullptr;
@@ -175,11 +188,11 @@ struct ScreenBuf {                                                    // one chu
         if (done) (void)hipEventDestroy(done);
     }
 };
-struct ScreenWs {                                                    // two chunks in flight + the rays' start
-    Stream st;
+struct ScreenWs {                                                    // chunks in flight + the rays' start
+    static constexpr int kSets = 3;
     HostBuf h_cam;
     void* d_cam = nullptr;
-    ScreenBuf buf[2];
+    ScreenBuf buf[kSets];
 };
 // A chunk's pixel table, then its first-pixel table (one entry per kScreenBlock rays).
 constexpr size_t kPixBytes = (size_t)kScreenMaxPix * sizeof(ScreenPix);
@@ -189,10 +202,10 @@ std::unique_ptr<ScreenWs> alloc_ws() {
     std::unique_ptr<ScreenWs> w(new ScreenWs());
     const size_t ray_bytes = (size_t)kScreenMaxRays * 3 * sizeof(double);
     const unsigned mapped = hipHostMallocMapped | hipHostMallocCoherent;
-    hipError_t e = hipStreamCreateWithFlags(&w->st.s, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipHostMalloc(&w->h_cam.p, 3 * sizeof(double), mapped);
+    hipError_t e = hipHostMalloc(&w->h_cam.p, 3 * sizeof(double), mapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer(&w->d_cam, w->h_cam.p, 0);
     for (ScreenBuf& b : w->buf) {
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&b.st.s, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipHostMalloc(&b.h_rgb.p, ray_bytes, mapped);
         if (e == hipSuccess) e = hipHostMalloc(&b.h_pix.p, kPixTableBytes, mapped);
         if (e == hipSuccess) e = hipHostMalloc(&b.h_jit.p, (size_t)kScreenMaxJit * 3 * sizeof(double), mapped);
@@ -267,16 +280,18 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // keeps resolving while the actual stream position drifts by up to kWin from the prediction (a count that
     // differs at an object edge no longer ends the chunk).  The jittered rays are formed on the device from the
     // chunk's randomUnit() values by the trace launch itself (rt_trace_screen_dev): the host generates each stream
-    // value once and sends 24 bytes per value instead of the rays, and a chunk is one launch.  Simulated on the reference's own sample counts (demo frame):
-    // 759 round trips instead of 2,515, for ~85 traced samples per pixel instead of 7.
+    // value once and sends 24 bytes per value instead of the rays, and a chunk is one launch.  Simulated on the
+    // reference's own sample counts (demo frame): 759 round trips instead of 2,515, for ~85 traced samples per pixel
+    // instead of 7 (tools/screen_sim.py replays the schedule).
     //
     // Two chunks in flight (r04).  While the GPU traces chunk c, the host builds and queues chunk c + 1 as the
     // continuation of c's prediction chain (the pixels below it that lie in c use c's predicted counts; its
     // stream base is c's predicted end minus kWin), then waits for c and resolves it.  When c resolves to its
     // end, c + 1 is already traced or tracing: the host's build and resolution overlap the GPU's round trip
-    // instead of following it.  When c breaks, c + 1 is dropped (its buffers are reused once the stream has
-    // passed it) and a chunk starts at the break, as before.  Resolution is unchanged: every pixel reads its
-    // samples at its actual stream position, or breaks.
+    // instead of following it.  When c breaks, c + 1 is dropped and a chunk starts at the break, as before.
+    // Chunks go to three buffer sets, each with its own stream: a dropped continuation finishes on its stream
+    // beside the restarted chain instead of ahead of it, and its set is reused once it is done.  Resolution is
+    // unchanged: every pixel reads its samples at its actual stream position, or breaks.
     const int kMaxRays = kScreenMaxRays, kMaxPix = kScreenMaxPix, kWin = 28;
     const int kMaxJit = kScreenMaxJit;
     static_assert(16 + 2 * kWin <= kScreenMaxWindow, "window longer than a pixel table entry allows");
@@ -286,16 +301,15 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // allocates its own.
     std::unique_ptr<ScreenWs> ws = take_ws(ctx);
     if (!ws) return rt_fail(RT_ENOMEM, "rt_render_screen: workspace allocation failed");
-    struct Give {                                                    // on every return: the stream's work is
+    struct Give {                                                    // on every return: the streams' work is
         rt_ctx* ctx;                                                 // done, then the workspace goes back
         std::unique_ptr<ScreenWs>& ws;
         ~Give() {
-            (void)hipStreamSynchronize(ws->st.s);
+            for (ScreenBuf& b : ws->buf) (void)hipStreamSynchronize(b.st.s);
             give_ws(ctx, std::move(ws));
         }
     } give{ctx, ws};
     ScreenBuf* buf = ws->buf;
-    Stream& st = ws->st;
     hipError_t e = hipSuccess;
     double* hc = static_cast<double*>(ws->h_cam.p);                  // the rays' start: the camera
     hc[0] = camera.x, hc[1] = camera.y, hc[2] = camera.z;
@@ -315,7 +329,8 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     int next_mul = 1;
     if (const char* ev = getenv("RT_SCREEN_NEXT")) next_mul = std::max(0, atoi(ev));
     using clk = std::chrono::steady_clock;
-    double t_build = 0, t_gpu = 0, t_res = 0;
+    double t_build = 0, t_gen = 0, t_gpu = 0, t_res = 0;
+    const auto t_start = clk::now();
     long long n_chunks = 0, n_rays = 0, n_dropped = 0;
 
     // A queued chunk: pixels p0 .. p0+m-1, windows relative to stream index S0.
@@ -377,9 +392,9 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
                                           static_cast<const ScreenPix*>(B.d_pix),
                                           reinterpret_cast<const int32_t*>(static_cast<const char*>(B.d_pix) + kPixBytes),
                                           m, static_cast<const double*>(B.d_jit), total, depth,
-                                          static_cast<double*>(B.d_rgb), st.s);
+                                          static_cast<double*>(B.d_rgb), B.st.s);
         if (r) return r;
-        const hipError_t er = hipEventRecord(B.done, st.s);
+        const hipError_t er = hipEventRecord(B.done, B.st.s);
         if (er != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(er));
         if (prof) {
             t_build += std::chrono::duration<double>(clk::now() - c0).count();
@@ -389,19 +404,42 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         return RT_OK;
     };
 
+    // A buffer set other than `a` whose last chunk is done: a dropped continuation drains on its own stream while
+    // the chain goes on in the other two sets (at most one set is draining).
+    auto pick = [&](int a, int* out) -> int {
+        int busy = -1;
+        for (int j = 1; j < ScreenWs::kSets; ++j) {
+            const int b = (a + j) % ScreenWs::kSets;
+            const hipError_t q = hipEventQuery(buf[b].done);
+            if (q == hipSuccess) {
+                *out = b;
+                return RT_OK;
+            }
+            if (q != hipErrorNotReady) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(q));
+            if (busy < 0) busy = b;
+        }
+        const hipError_t q = hipEventSynchronize(buf[busy].done);
+        if (q != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(q));
+        *out = busy;
+        return RT_OK;
+    };
+
     Chunk cur, nxt;
     if ((rc = queue(cur, 0, 0, 0, 0, walk, chunk))) return rc;
     while (p < P) {
         // the continuation of cur's prediction chain, queued behind it
         bool have_next = false;
         if (next_mul > 0 && cur.p0 + cur.m < P) {
-            if ((rc = queue(nxt, cur.b ^ 1, cur.p0 + cur.m, cur.S0 + (uint64_t)cur.spred_end, S, cur.walk_end,
+            int nb = 0;
+            if ((rc = pick(cur.b, &nb))) return rc;
+            if ((rc = queue(nxt, nb, cur.p0 + cur.m, cur.S0 + (uint64_t)cur.spred_end, S, cur.walk_end,
                             std::min(chunk * next_mul, kMaxPix))))
                 return rc;
             have_next = true;
         }
         // While the GPU traces: generate the stream values the following chunk will need (rand() + normalize
         // are the host's largest share of a round trip), so its build only copies them.
+        const auto cg = clk::now();
         jit.ensure(have_next ? nxt.jend + (nxt.jend - nxt.S0) + 64 : cur.jend + 64);
         const auto c1 = clk::now();
         e = hipEventSynchronize(buf[cur.b].done);
@@ -459,6 +497,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         if (q > 0) S = cur.S0 + (uint64_t)A;                         // (q == 0: nothing resolved, S unchanged)
         jit.consume_until(S);
         if (prof) {
+            t_gen += std::chrono::duration<double>(c1 - cg).count();
             t_gpu += std::chrono::duration<double>(c2 - c1).count();
             t_res += std::chrono::duration<double>(clk::now() - c2).count();
         }
@@ -471,20 +510,16 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
             }
             continue;
         }
-        // cur broke at pixel p: restart the chain there (in cur's buffers, free now) and drop the queued
-        // continuation, whose buffers the next continuation rewrites once the stream has passed it
+        // cur broke at pixel p: restart the chain there (in cur's buffers and stream, free now); the queued
+        // continuation is dropped and finishes on its own stream, beside the restarted chain, not ahead of it
         chunk = std::max(16, chunk / 2);
-        const int dropped = have_next ? nxt.b : -1;
+        if (have_next) ++n_dropped;
         if (p < P && (rc = queue(cur, cur.b, p, S, S, walk, chunk))) return rc;
-        if (dropped >= 0) {
-            ++n_dropped;
-            e = hipEventSynchronize(buf[dropped].done);
-            if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(e));
-        }
     }
     if (prof)
-        fprintf(stderr, "rt_render_screen: %lld chunks (%lld dropped), %lld rays traced; build %.1f ms, gpu wait %.1f ms, "
-                "resolve %.1f ms\n", n_chunks, n_dropped, n_rays, t_build * 1e3, t_gpu * 1e3, t_res * 1e3);
+        fprintf(stderr, "rt_render_screen: %lld chunks (%lld dropped), %lld rays traced; build %.1f ms, %llu stream values "
+                "%.1f ms, gpu wait %.1f ms, resolve %.1f ms; loop %.1f ms\n", n_chunks, n_dropped, n_rays, t_build * 1e3,
+                (unsigned long long)(jit.base + jit.n), t_gen * 1e3, t_gpu * 1e3, t_res * 1e3, std::chrono::duration<double>(clk::now() - t_start).count() * 1e3);
     if (rand_calls) *rand_calls = jit.consumed_calls;
     return RT_OK;
 }

@@ -36,6 +36,7 @@ hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned int) {
 }
 hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
 hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventQuery(hipEvent_t) { return hipSuccess; }
 hipError_t hipEventDestroy(hipEvent_t e) {
     delete reinterpret_cast<int*>(e);
     return hipSuccess;
