@@ -324,7 +324,8 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
         dm[m].reflect = reflect ? 1 : 0;
     }
 
-    const size_t bytes = (size_t)rt::scene_bytes_for(s->n_spheres, s->n_meshes, n_tris, s->n_lights);
+    // (rounded up to 16 B: kernels may copy the whole record into LDS in 4- or 16-byte words)
+    const size_t bytes = ((size_t)rt::scene_bytes_for(s->n_spheres, s->n_meshes, n_tris, s->n_lights) + 15) & ~(size_t)15;
     const int np = rt::padded_spheres(s->n_spheres);
     const int ns = rt::sphere_stride(np);            // array stride (rt_layout.hpp)
     blob->assign(bytes, 0);

@@ -1115,6 +1115,8 @@ extern "C" int rt_host_free(void* p) {
     return RT_OK;
 }
 
+constexpr size_t kScreenLdsMax = 64 * 1024;       // screen chunks: scene record in LDS when it fits beside the slots
+
 static int trace_rays_launch(rt_ctx* c, const double* starts, const double* ends, int n, int depth, double* rgb64f,
                              uint32_t* raycount, hipStream_t st, const ScreenArgs& sa) {
     RT_HIP(hipSetDevice(c->device));
@@ -1151,6 +1153,10 @@ int rt_trace_screen_dev(rt_ctx* c, const double cam[3], const ScreenPix* pix, co
     if (n <= 0 || m <= 0) return RT_OK;
     ScreenArgs sa;
     sa.pix = pix, sa.m = m, sa.first = first, sa.jit = jit;
+    // RT_SCREEN_LDS=0 (A/B): the scene record read from global memory instead of LDS
+    static const bool lds = !getenv("RT_SCREEN_LDS") || atoi(getenv("RT_SCREEN_LDS")) != 0;
+    const size_t slots = c->tree ? 0 : slot_bytes(depth, c->transparent);
+    if (lds && c->scene_bytes % 8 == 0 && (size_t)c->scene_bytes + slots <= kScreenLdsMax) sa.scene_lds = c->scene_bytes;
     return trace_rays_launch(c, cam, nullptr, n, depth, rgb64f, nullptr, (hipStream_t)stream, sa);
 }
 

@@ -437,12 +437,24 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
                                                                  uint32_t* __restrict__ rc,
                                                                  const ScreenPix* __restrict__ spix, int sm,
                                                                  const int32_t* __restrict__ sfirst,
-                                                                 const double* __restrict__ sjit) {
+                                                                 const double* __restrict__ sjit, int scene_lds) {
     static_assert(kThreads == kScreenBlock, "one first-pixel entry per workgroup");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // Every lane traces (trace() reduces over the wave); lanes past n repeat ray n - 1 and store nothing.
     const int k = blockIdx.x * kThreads + threadIdx.x, kk = k < n ? k : n - 1;
     uint32_t seg = 0, sh = 0;
+    // scene_lds > 0 (small launches: rt_render_screen's chunks): the whole scene record is copied into LDS first —
+    // one burst of loads instead of a cold-cache round trip per record on the rays' dependent chain.  (The slots
+    // behind it stay 8-byte aligned: scene_lds is a multiple of 8.)
+    int off = 0;
+    if (scene_lds > 0) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(S);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
+        for (int q = threadIdx.x; q < (scene_lds >> 2); q += kThreads) dst[q] = src[q];
+        __syncthreads();
+        S = reinterpret_cast<const DevScene*>(smem);
+        off = scene_lds;
+    }
     SceneView V = view_of(S, S, S->n_padded, S->n_stride, S->n_lights);
     d3 p0, p1;
     if (spix) {
@@ -457,8 +469,8 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
         p1 = ld3(ends + 3 * kk);
     }
     V.hits_ok = hits_ok_from(S, p0);
-    double* slot = reinterpret_cast<double*>(smem) + threadIdx.x;
-    int* mslot = reinterpret_cast<int*>(smem + 3 * 8 * colour_slots(B, TRANSP) * kSlotStride) + threadIdx.x;
+    double* slot = reinterpret_cast<double*>(smem + off) + threadIdx.x;
+    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * colour_slots(B, TRANSP) * kSlotStride) + threadIdx.x;
     d3 c;
     if constexpr (TREE)
         c = trace_tree<B>(V, p0, p1, &seg, &sh);
@@ -475,6 +487,7 @@ struct ScreenArgs {
     int m = 0;
     const int32_t* first = nullptr;
     const double* jit = nullptr;
+    int scene_lds = 0;                 // bytes of the scene record copied into LDS (multiple of 4; 0: none)
 };
 
 // Render-kernel variants rt_render_dev chooses between (rt_kernel.hip).
@@ -592,15 +605,16 @@ hipError_t launch_trace_rays_impl(int variant, dim3 grid, hipStream_t st, const 
     if constexpr (B > RT_MAX_B) {
         return hipErrorInvalidValue;
     } else {
+        const size_t lds = (size_t)sa.scene_lds;
         if (variant == 2)
-            hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, true>), grid, dim3(kThreads), 0, st, s, a, b, n, rgb, rc,
-                               sa.pix, sa.m, sa.first, sa.jit);
+            hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, true>), grid, dim3(kThreads), lds, st, s, a, b, n, rgb, rc,
+                               sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
         else if (variant == 1)
-            hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, false>), grid, dim3(kThreads), slot_bytes(B, true), st, s,
-                               a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit);
+            hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, false>), grid, dim3(kThreads), lds + slot_bytes(B, true),
+                               st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
         else
-            hipLaunchKernelGGL((rt_trace_rays_kernel<B, false, false>), grid, dim3(kThreads), slot_bytes(B, false), st,
-                               s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit);
+            hipLaunchKernelGGL((rt_trace_rays_kernel<B, false, false>), grid, dim3(kThreads), lds + slot_bytes(B, false),
+                               st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
         return hipGetLastError();
     }
 }

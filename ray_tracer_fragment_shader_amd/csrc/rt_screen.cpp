@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -179,6 +180,7 @@ struct Stream {
 
 struct ScreenBuf {                                                    // one chunk's stream and mapped buffers
     Stream st;
+    std::vector<double> sp;                                          // host: screen point of each pixel (x, y, z)
     HostBuf h_rgb, h_pix, h_jit;
     void* d_rgb = nullptr;
     void* d_pix = nullptr;
@@ -189,7 +191,8 @@ struct ScreenBuf {                                                    // one chu
     }
 };
 struct ScreenWs {                                                    // chunks in flight + the rays' start
-    static constexpr int kSets = 3;
+    static constexpr int kAheadMax = 2;                              // continuations queued behind a chunk
+    static constexpr int kSets = 2 * kAheadMax + 1;                  // in flight + draining
     HostBuf h_cam;
     void* d_cam = nullptr;
     ScreenBuf buf[kSets];
@@ -206,6 +209,7 @@ std::unique_ptr<ScreenWs> alloc_ws() {
     if (e == hipSuccess) e = hipHostGetDevicePointer(&w->d_cam, w->h_cam.p, 0);
     for (ScreenBuf& b : w->buf) {
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&b.st.s, hipStreamNonBlocking);
+        b.sp.resize(3 * (size_t)kScreenMaxPix);
         if (e == hipSuccess) e = hipHostMalloc(&b.h_rgb.p, ray_bytes, mapped);
         if (e == hipSuccess) e = hipHostMalloc(&b.h_pix.p, kPixTableBytes, mapped);
         if (e == hipSuccess) e = hipHostMalloc(&b.h_jit.p, (size_t)kScreenMaxJit * 3 * sizeof(double), mapped);
@@ -328,6 +332,10 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // chunk in flight as in r03).
     int next_mul = 1;
     if (const char* ev = getenv("RT_SCREEN_NEXT")) next_mul = std::max(0, atoi(ev));
+    // RT_SCREEN_AHEAD (A/B): continuations kept queued behind the chunk being resolved (1: r04's two chunks in flight).
+    int ahead = 1;
+    if (const char* ev = getenv("RT_SCREEN_AHEAD")) ahead = atoi(ev);
+    ahead = next_mul > 0 ? std::min(std::max(ahead, 1), ScreenWs::kAheadMax) : 0;
     using clk = std::chrono::steady_clock;
     double t_build = 0, t_gen = 0, t_gpu = 0, t_res = 0;
     const auto t_start = clk::now();
@@ -342,7 +350,6 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         long long spred_end = 0;                                     // predicted start of pixel p0+m, rel. to S0
         uint64_t jend = 0;                                           // its stream values: S0 .. jend - 1
         V3 walk_end = v3(0.0, 0.0, 0.0);                             // screen point of pixel p0+m
-        std::vector<V3> sp;                                          // screen point of each pixel
     };
     // Build chunk (pixels p0.., at most `want`) into buffer set b and queue its round trip.  pred_start: the
     // predicted first sample of pixel p0 (absolute); the chunk's base is pred_start - kWin, at least `floor`.
@@ -355,7 +362,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         c.b = b;
         c.p0 = p0;
         c.S0 = std::max<uint64_t>(floor, pred_start > (uint64_t)kWin ? pred_start - kWin : 0);
-        c.sp.resize(kMaxPix);
+        double* sp = B.sp.data();
         int m = (int)std::min<long long>(want, P - p0);
         V3 w = w0;
         int total = 0, jmax = 0, nb = 0;
@@ -371,7 +378,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
                 break;
             }
             pcount[pix] = (uint8_t)pred;
-            c.sp[q] = w;
+            sp[3 * q] = w.x, sp[3 * q + 1] = w.y, sp[3 * q + 2] = w.z;
             hp[q].sp[0] = w.x, hp[q].sp[1] = w.y, hp[q].sp[2] = w.z;
             hp[q].base = (int32_t)lo, hp[q].len = len, hp[q].off = total, hp[q].pad = 0;
             for (; nb * kScreenBlock < total + len; ++nb) hf[nb] = q;  // workgroups whose first ray is q's
@@ -404,44 +411,54 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         return RT_OK;
     };
 
-    // A buffer set other than `a` whose last chunk is done: a dropped continuation drains on its own stream while
-    // the chain goes on in the other two sets (at most one set is draining).
-    auto pick = [&](int a, int* out) -> int {
-        int busy = -1;
-        for (int j = 1; j < ScreenWs::kSets; ++j) {
-            const int b = (a + j) % ScreenWs::kSets;
+    // A buffer set no queued chunk uses, preferably one whose last chunk is done (dropped continuations drain on
+    // their own streams while the chain goes on in the other sets).
+    bool in_use[ScreenWs::kSets] = {};
+    auto pick = [&](int* out) -> int {
+        int idle = -1;
+        for (int b = 0; b < ScreenWs::kSets; ++b) {
+            if (in_use[b]) continue;
             const hipError_t q = hipEventQuery(buf[b].done);
             if (q == hipSuccess) {
                 *out = b;
                 return RT_OK;
             }
             if (q != hipErrorNotReady) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(q));
-            if (busy < 0) busy = b;
+            if (idle < 0) idle = b;
         }
-        const hipError_t q = hipEventSynchronize(buf[busy].done);
+        const hipError_t q = hipEventSynchronize(buf[idle].done);   // (kSets > 1 + kAheadMax: one exists)
         if (q != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(q));
-        *out = busy;
+        *out = idle;
         return RT_OK;
     };
+    auto queue_in_free = [&](std::deque<Chunk>& fl, long long p0, uint64_t pred_start, uint64_t floor, V3 w0,
+                             int want) -> int {
+        int b = 0;
+        int r = pick(&b);
+        if (!r) {
+            fl.emplace_back();
+            r = queue(fl.back(), b, p0, pred_start, floor, w0, want);
+            if (!r) in_use[b] = true;
+        }
+        return r;
+    };
 
-    Chunk cur, nxt;
-    if ((rc = queue(cur, 0, 0, 0, 0, walk, chunk))) return rc;
+    std::deque<Chunk> fl;                                            // chunks in flight, oldest first
+    if ((rc = queue_in_free(fl, 0, 0, 0, walk, chunk))) return rc;
     while (p < P) {
-        // the continuation of cur's prediction chain, queued behind it
-        bool have_next = false;
-        if (next_mul > 0 && cur.p0 + cur.m < P) {
-            int nb = 0;
-            if ((rc = pick(cur.b, &nb))) return rc;
-            if ((rc = queue(nxt, nb, cur.p0 + cur.m, cur.S0 + (uint64_t)cur.spred_end, S, cur.walk_end,
-                            std::min(chunk * next_mul, kMaxPix))))
+        // continuations of the prediction chain, queued behind the chunk about to be resolved
+        while ((int)fl.size() < 1 + ahead && fl.back().p0 + fl.back().m < P) {
+            const Chunk t = fl.back();
+            if ((rc = queue_in_free(fl, t.p0 + t.m, t.S0 + (uint64_t)t.spred_end, S, t.walk_end,
+                                    std::min(chunk * next_mul, kMaxPix))))
                 return rc;
-            have_next = true;
         }
         // While the GPU traces: generate the stream values the following chunk will need (rand() + normalize
         // are the host's largest share of a round trip), so its build only copies them.
         const auto cg = clk::now();
-        jit.ensure(have_next ? nxt.jend + (nxt.jend - nxt.S0) + 64 : cur.jend + 64);
+        jit.ensure(fl.back().jend + (fl.back().jend - fl.back().S0) + 64);
         const auto c1 = clk::now();
+        const Chunk cur = fl.front();
         e = hipEventSynchronize(buf[cur.b].done);
         if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(e));
         const auto c2 = clk::now();
@@ -490,7 +507,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
             if (samples) samples[pix] = (uint8_t)n;
             counts[pix] = (uint8_t)n;
             A += n;
-            walk = cur.sp[q] + right;
+            walk = v3(&buf[cur.b].sp[3 * q]) + right;
             if ((int)(pix % W) == W - 1) walk = (walk - rightOffset) + up;
         }
         p = cur.p0 + q;
@@ -501,20 +518,20 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
             t_gpu += std::chrono::duration<double>(c2 - c1).count();
             t_res += std::chrono::duration<double>(clk::now() - c2).count();
         }
+        in_use[cur.b] = false;
+        fl.pop_front();
         if (!broke && q == cur.m) {
             chunk = std::min(kMaxPix, chunk * 2);
-            if (have_next) {
-                std::swap(cur, nxt);                                 // already queued at the right place
-            } else if (p < P && (rc = queue(cur, cur.b, p, S, S, walk, chunk))) {
-                return rc;
-            }
+            if (fl.empty() && p < P && (rc = queue_in_free(fl, p, S, S, walk, chunk))) return rc;
             continue;
         }
-        // cur broke at pixel p: restart the chain there (in cur's buffers and stream, free now); the queued
-        // continuation is dropped and finishes on its own stream, beside the restarted chain, not ahead of it
+        // cur broke at pixel p: the queued continuations are dropped (each finishes on its own stream, beside the
+        // restarted chain, not ahead of it) and the chain restarts there
         chunk = std::max(16, chunk / 2);
-        if (have_next) ++n_dropped;
-        if (p < P && (rc = queue(cur, cur.b, p, S, S, walk, chunk))) return rc;
+        n_dropped += (long long)fl.size();
+        for (const Chunk& d : fl) in_use[d.b] = false;
+        fl.clear();
+        if (p < P && (rc = queue_in_free(fl, p, S, S, walk, chunk))) return rc;
     }
     if (prof)
         fprintf(stderr, "rt_render_screen: %lld chunks (%lld dropped), %lld rays traced; build %.1f ms, %llu stream values "
