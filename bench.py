@@ -342,7 +342,7 @@ def packed_host_legs(t, sa, cam, W, H, B, k=30):
             out[key] = round((time.perf_counter() - t0) / k * 1e3, 4)
         out["packed_note"] = ("c2 frame as GRAY8 (2.07 MB: the scene is achromatic, rt_scene_achromatic) into pinned "
                               "memory: synchronous per call (render + copy kernel on the render stream), and pipelined "
-                              "(queue frame f, wait for frame f-1 — one frame of latency — or f-2: the SDMA copy of a "
+                              "(queue frame f, wait for frame f-1 — one frame of latency — or f-2: the copy kernel of a "
                               "frame on the copy stream runs beside the next frame's render)")
     finally:
         for p in pins:

@@ -238,7 +238,7 @@ int rt_render_dev_packed(rt_ctx* ctx, const rt_camera* cam, int width, int heigh
 /* Host-buffer frames in one format (draw()'s replacement with fewer PCIe bytes).  rt_render_packed is
  * synchronous (stats nullable, as rt_render): the render and a copy kernel that writes the frame over PCIe
  * into host_pixels, back to back on the context's render stream.  rt_render_packed_async queues the render
- * on the render stream and the device-to-host copy as an SDMA transfer on the context's copy stream, and
+ * on the render stream and the device-to-host copy kernel on the context's copy stream, and
  * returns at once with a ticket: the copy of frame t runs beside the render of frame t+1 (three device
  * buffers: up to two frames may be waited for behind the one being queued); rt_ctx_wait(ctx, t) returns
  * when frame t's pixels are in host_pixels (ticket 0: everything queued).  host_pixels must stay valid until

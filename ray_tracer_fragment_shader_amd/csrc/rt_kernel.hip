@@ -288,8 +288,7 @@ __global__ __launch_bounds__(kThreads) void rt_unpack_kernel(const uint8_t* __re
 // sums[0], sums[1] (zeroed by the caller), so only 16 bytes cross PCIe instead of 4 bytes per pixel.
 // Device -> pinned host frame (rt_host_alloc memory, mapped into the device's address space): a copy kernel
 // whose 16-byte stores cross PCIe straight into the host buffer.  On the render stream it needs no cross-stream
-// hand-off, and unlike hipMemcpyAsync's SDMA path (measured on MI355X: 0.20-0.48 ms per c2 GRAY8 frame once
-// copies overlap renders, against 0.08 ms with copy kernels) it overlaps the next frame's render.
+// hand-off; on the copy stream it overlaps the next frame's render (rt_ctx::copy_mode has the measurements).
 __global__ __launch_bounds__(kThreads) void rt_copy_out_kernel(const uint8_t* __restrict__ src,
                                                                uint8_t* __restrict__ dst, size_t n) {
     const size_t n16 = n >> 4;
@@ -371,19 +370,23 @@ struct rt_ctx {
     int use_lds = 0;                           // RT_SCENE_IN_LDS=1: header + exact records in LDS (A/B: tools/ab.py)
     int wg_staging = 0;                        // RT_WG_STAGING=1: LDS-staged 32-pixel row stores (A/B)
     // Where the packed host frames' device-to-host copy runs (r04, tools/copy_ab.py and tools/copy_trace.py on MI355X,
-    // c2 GRAY8, 2.07 MB into pinned memory; us per frame):
-    //                                          synchronous   pipelined (wait f-1)   (wait f-2)
-    //   copy kernel behind the render (rs)         85              74                 74
-    //   copy kernel on the copy stream (cs)       100              75                 72   (16 workgroups: 66)
-    //   SDMA (hipMemcpyAsync) on the copy stream  107              59-60              59
-    // A copy kernel running beside the next render slows both (kernel trace: render 36 -> 60 us, copy 38 -> 55 us);
-    // the SDMA engines take no CUs.  So rt_render_packed (synchronous) queues a copy kernel behind the render on
-    // `rs`, and rt_render_packed_async an SDMA copy on `cs` after a cross-stream event.  RT_COPY_MODE (1: rs,
-    // 0: cs, 2: the kernel stores straight into the pinned buffer — 290 us: single-byte stores over PCIe) and
-    // RT_COPY_KERNEL (1: copy kernel, 0: SDMA) force one choice for both calls (A/B; -1: the defaults above).
+    // c2 GRAY8, 2.07 MB into pinned memory; us per frame, medians of 5 interleaved rounds x 60 frames):
+    //                                              synchronous   pipelined (wait f-1)   (wait f-2)
+    //   copy kernel behind the render (rs)             84-85         74-75               74-75
+    //   copy kernel on the copy stream (cs), 16 WGs    100           74                  66
+    //                                     4 / 8 WGs    122 / 108     111 / 77            111 / 64
+    //   hipMemcpyAsync on the copy stream              106-107       59 / 95 / 290       59 / 95 / 290
+    // The runtime executes that hipMemcpyAsync as its own blit kernel (__amd_rocclr_copyBuffer in the kernel trace, no
+    // SDMA transfer in the memory-copy trace, whatever GPU_FORCE_BLIT_COPY_SIZE / ROC_ENABLE_LARGE_BAR /
+    // HSA_ENABLE_SDMA / GPU_BLIT_ENGINE_TYPE say), and its pipelined rate settles in one of three states per process
+    // (59, 95 or 290 us) — so the product uses its own copy kernel for both calls: behind the render on `rs` for
+    // rt_render_packed, on `cs` with 16 workgroups (a copy beside the next render takes CUs from it: fewer
+    // workgroups leave it more) after a cross-stream event for rt_render_packed_async.  RT_COPY_MODE (1: rs, 0: cs,
+    // 2: the kernel stores straight into the pinned buffer — 290 us: single-byte stores over PCIe), RT_COPY_KERNEL
+    // (0: hipMemcpyAsync) and RT_COPY_BLOCKS override (A/B; -1 / 0: the defaults above).
     int copy_mode = -1;
     int copy_kernel = -1;
-    int copy_blocks = 0;                       // RT_COPY_BLOCKS: workgroups of the copy kernel (0: one per 4 KB, <= 1024)
+    int copy_blocks = 0;                       // RT_COPY_BLOCKS: workgroups of the copy kernel (0: the defaults above)
     // Adaptive tile-row order (rt_order_kernel): the first render of a new (scene, camera, size, rows,
     // depth, outputs) view uses the identity order; the second render of the same view is a calibration
     // render that also times its tile rows; later renders dispatch the rows by decreasing time.  A render
@@ -937,14 +940,18 @@ static void* pinned_device_ptr(const void* host, size_t bytes) {
     return (void*)(it->second.second + (h - it->first));
 }
 
-// kernel: copy kernel into rt_host_alloc memory (else hipMemcpyAsync); RT_COPY_KERNEL overrides.
-static int copy_to_host(rt_ctx* c, void* host, const void* dev, size_t bytes, hipStream_t st, bool kernel = true) {
+constexpr unsigned kCopyStreamBlocks = 16;     // copy kernel beside a render: workgroups (rt_ctx::copy_mode)
+
+// A copy kernel into rt_host_alloc memory (else hipMemcpyAsync); max_blocks: its workgroups (0: one per 4 KB, up to
+// 1024).  RT_COPY_KERNEL / RT_COPY_BLOCKS override.
+static int copy_to_host(rt_ctx* c, void* host, const void* dev, size_t bytes, hipStream_t st, unsigned max_blocks = 0) {
     if (!bytes) return RT_OK;
     void* dmap = pinned_device_ptr(host, bytes);
-    if (c->copy_kernel >= 0) kernel = c->copy_kernel != 0;
+    const bool kernel = c->copy_kernel != 0;
     if (dmap && kernel && ((uintptr_t)dmap | (uintptr_t)dev) % 16 == 0) {
         unsigned blocks = (unsigned)std::min<size_t>((bytes / 16 + kThreads - 1) / kThreads + 1, 1024);
-        if (c->copy_blocks > 0) blocks = std::min(blocks, (unsigned)c->copy_blocks);
+        if (c->copy_blocks > 0) max_blocks = (unsigned)c->copy_blocks;
+        if (max_blocks > 0) blocks = std::min(blocks, max_blocks);
         hipLaunchKernelGGL(rt_copy_out_kernel, dim3(blocks), dim3(kThreads), 0, st, (const uint8_t*)dev,
                            (uint8_t*)dmap, bytes);
         RT_HIP(hipGetLastError());
@@ -993,7 +1000,7 @@ extern "C" int rt_render(rt_ctx* c, const rt_scene* scene, const rt_camera* cam,
 }
 
 // rt_render_packed / rt_render_packed_async: one image in `format`, copied to host memory.
-// async: the copy goes to the copy stream as an SDMA transfer (pipelined frames), else a copy kernel behind the
+// async: the copy kernel goes to the copy stream (pipelined frames: it runs beside the next render), else behind the
 // render on the render stream (see rt_ctx::copy_mode).
 static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera* cam, int W, int H, int depth,
                                int format, void* host, int slot, bool with_stats, size_t* npx_out, void** sums,
@@ -1036,7 +1043,7 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
         RT_HIP(hipEventRecord(c->rendered[slot], c->rs));
         RT_HIP(hipStreamWaitEvent(cs, c->rendered[slot], 0));
     }
-    if (!direct && (rc = copy_to_host(c, host, px, npx * pb, cs, !async))) return rc;
+    if (!direct && (rc = copy_to_host(c, host, px, npx * pb, cs, mode == 0 ? kCopyStreamBlocks : 0))) return rc;
     RT_HIP(hipEventRecord(c->copied[slot], cs));
     c->copied_rec[slot] = true;
     c->copied_cs[slot] = cs != c->rs;

@@ -20,7 +20,7 @@ from ray_tracer_fragment_shader_amd import abi, scenes  # noqa: E402
 from ray_tracer_fragment_shader_amd.tracer import Tracer  # noqa: E402
 
 SETTINGS = [tuple(x.split(":")) for x in os.environ.get("SETTINGS", "1:0,0:0,0:64,0:16,1:64,2:0").split(",")]
-# (RT_COPY_KERNEL=0 in the environment: hipMemcpyAsync (SDMA) instead of the copy kernel)
+# (RT_COPY_KERNEL=0 in the environment: hipMemcpyAsync — the runtime's blit kernel — instead of the copy kernel)
 L = abi.lib()
 cfg = scenes.CONFIGS["c2"]
 W, H, B = cfg.width, cfg.height, cfg.depth

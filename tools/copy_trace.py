@@ -55,7 +55,7 @@ def parse(d):
     ren = sorted([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
                   if "rt_render_kernel" in r["Kernel_Name"]])[-30:]
     cop = sorted([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
-                  if "rt_copy_out_kernel" in r["Kernel_Name"]])[-30:]
+                  if "rt_copy_out_kernel" in r["Kernel_Name"] or "copyBuffer" in r["Kernel_Name"]])[-30:]
     mc = glob.glob(d + "/**/*memory_copy_trace.csv", recursive=True)
     if not cop and mc:                                       # SDMA copies (--memory-copy-trace)
         cop = sorted([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(mc[0]))
