@@ -94,13 +94,15 @@
 // The skips in the fast (non-CULL) bounce loop from this depth on (they always run in the CULL variant).
 // There they come with the continuation parked in LDS across the light loop (RT_PARK_ND): without it the
 // extra live state spilled 12 B/lane at 6 waves/SIMD (c2 HBM writes 1.01x -> 1.22x); with it no spills,
-// c3 (depth 2) -1.2 to -1.9%, c2 (depth 1) +0.7 to +1.1% (in-process A/B) — hence depth >= 2.
+// c3 (depth 2) -1.2 to -1.9%, c2 (depth 1) +0.7 to +1.1% (r02, in-process A/B) — hence depth >= 2 until r04.  The
+// 7-wave depth-1 kernel (94 SGPRs, 65 VGPRs, no scratch) gains from them: c2 -1.9% serial, -0.5% with 3 frames
+// in flight (r04, in-process A/B; the skips alone -1.4%, the parking alone +0.8%) — hence depth >= 1.
 // 1: primary rays of waves whose cone mask keeps no sphere normalise their direction only where they hit the board.
 #ifndef RT_LAZY_PRIMARY_U
 #define RT_LAZY_PRIMARY_U 1
 #endif
 #ifndef RT_SKIP_FAST_MIN_B
-#define RT_SKIP_FAST_MIN_B 2
+#define RT_SKIP_FAST_MIN_B 1
 #endif
 
 // 1: diagnostic build (tools/counters.py): wave-level event counters in DevScene::counters.
