@@ -242,11 +242,11 @@ def kernel_rooflines(cfg_name, nl, W, H, avg_kern_ms):
              "reference_flops_per_launch": ref_flops})
 
 
-ROCPROF_ONE_STREAM = "profiles/r03/{cfg}_kernel_stats_1stream.csv"
+ROCPROF_ONE_STREAM = "profiles/r04/{cfg}_kernel_stats_1stream.csv"
 
 
 def rocprof_reference(cfg_name, full_frame):
-    """The committed one-stream rocprofv3 --kernel-trace --stats summary of this config (PROFILE=1 tools/gpu_r03.sh:
+    """The committed one-stream rocprofv3 --kernel-trace --stats summary of this config (tools/gpu_r04_prof.sh:
     bench.py --frames-in-flight 1 --profile-kernel-only): AverageNs of rt_render_kernel is the launch duration,
     so bytes / AverageNs / peak reproduces `frac` from profiles/ alone."""
     path = os.path.join(ROOT, ROCPROF_ONE_STREAM.format(cfg=cfg_name))
