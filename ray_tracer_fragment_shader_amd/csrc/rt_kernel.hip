@@ -1162,7 +1162,7 @@ int rt_trace_screen_dev(rt_ctx* c, const double cam[3], const ScreenPix* pix, co
     sa.pix = pix, sa.m = m, sa.first = first, sa.jit = jit;
     // RT_SCREEN_LDS=0 (A/B): the scene record read from global memory instead of LDS
     static const bool lds = !getenv("RT_SCREEN_LDS") || atoi(getenv("RT_SCREEN_LDS")) != 0;
-    const size_t slots = c->tree ? 0 : slot_bytes(depth, c->transparent);
+    const size_t slots = c->tree ? 0 : slot_bytes(depth, c->transparent, kScreenBlock);
     if (lds && c->scene_bytes % 8 == 0 && (size_t)c->scene_bytes + slots <= kScreenLdsMax) sa.scene_lds = c->scene_bytes;
     return trace_rays_launch(c, cam, nullptr, n, depth, rgb64f, nullptr, (hipStream_t)stream, sa);
 }

@@ -168,4 +168,9 @@ struct ScreenPix {
     int32_t base, len, off, pad;
 };
 constexpr int kScreenMaxWindow = 128;          // len <= this
-constexpr int kScreenBlock = 256;              // rays per first-pixel table entry (the trace kernel's workgroup)
+// (64-thread workgroups — one wave per CU for a small chunk — measured the same GPU wait per chunk as 256: the
+// latency is the trace's own instruction chain, not CU sharing)
+#ifndef RT_SCREEN_WG
+#define RT_SCREEN_WG 256
+#endif
+constexpr int kScreenBlock = RT_SCREEN_WG;     // rays per first-pixel table entry (the screen trace launch's workgroup)

@@ -429,8 +429,8 @@ void rt_render_kernel_sg(const DevScene* __restrict__ gscene, RenderParams P, vo
 // points may skip the bounding-sphere cull is decided per ray (hits_ok_from).
 // Screen mode (spix != nullptr, rt_render_screen's chunks): every ray starts at starts[0..2] (the camera) and ends at
 // its pixel's screen point + 0.5 * its jitter value (MSA:1296), formed here instead of by a launch of its own.
-template <int B, bool TRANSP, bool TREE = false>
-__global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene* __restrict__ S,
+template <int B, bool TRANSP, bool TREE = false, int WG = kThreads>
+__global__ __launch_bounds__(WG) void rt_trace_rays_kernel(const DevScene* __restrict__ S,
                                                                  const double* __restrict__ starts,
                                                                  const double* __restrict__ ends, int n,
                                                                  double* __restrict__ rgb,
@@ -438,10 +438,9 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
                                                                  const ScreenPix* __restrict__ spix, int sm,
                                                                  const int32_t* __restrict__ sfirst,
                                                                  const double* __restrict__ sjit, int scene_lds) {
-    static_assert(kThreads == kScreenBlock, "one first-pixel entry per workgroup");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // Every lane traces (trace() reduces over the wave); lanes past n repeat ray n - 1 and store nothing.
-    const int k = blockIdx.x * kThreads + threadIdx.x, kk = k < n ? k : n - 1;
+    const int k = blockIdx.x * WG + threadIdx.x, kk = k < n ? k : n - 1;
     uint32_t seg = 0, sh = 0;
     // scene_lds > 0 (small launches: rt_render_screen's chunks): the whole scene record is copied into LDS first —
     // one burst of loads instead of a cold-cache round trip per record on the rays' dependent chain.  (The slots
@@ -450,7 +449,7 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
     if (scene_lds > 0) {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(S);
         uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
-        for (int q = threadIdx.x; q < (scene_lds >> 2); q += kThreads) dst[q] = src[q];
+        for (int q = threadIdx.x; q < (scene_lds >> 2); q += WG) dst[q] = src[q];
         __syncthreads();
         S = reinterpret_cast<const DevScene*>(smem);
         off = scene_lds;
@@ -459,7 +458,7 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
     d3 p0, p1;
     if (spix) {
         p0 = ld3(starts);
-        int q = sfirst[blockIdx.x];                         // the pixel of the workgroup's first ray
+        int q = sfirst[blockIdx.x];                         // the pixel of the workgroup's first ray (WG = kScreenBlock)
         while (q + 1 < sm && spix[q + 1].off <= kk) ++q;
         const ScreenPix& X = spix[q];
         const double* J = sjit + 3 * (size_t)(X.base + (kk - X.off));
@@ -470,12 +469,12 @@ __global__ __launch_bounds__(kThreads) void rt_trace_rays_kernel(const DevScene*
     }
     V.hits_ok = hits_ok_from(S, p0);
     double* slot = reinterpret_cast<double*>(smem + off) + threadIdx.x;
-    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * colour_slots(B, TRANSP) * kSlotStride) + threadIdx.x;
+    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * colour_slots(B, TRANSP) * WG) + threadIdx.x;
     d3 c;
     if constexpr (TREE)
         c = trace_tree<B>(V, p0, p1, &seg, &sh);
     else
-        c = trace<B, false, TRANSP, false>(V, p0, p1, ~0ull, &seg, &sh, slot, mslot);
+        c = trace<B, false, TRANSP, false, WG>(V, p0, p1, ~0ull, &seg, &sh, slot, mslot);
     if (k >= n) return;
     if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
     if (rc) rc[k] = seg | (sh << 16);
@@ -606,6 +605,20 @@ hipError_t launch_trace_rays_impl(int variant, dim3 grid, hipStream_t st, const 
         return hipErrorInvalidValue;
     } else {
         const size_t lds = (size_t)sa.scene_lds;
+        if (sa.pix) {                                   // screen chunks: kScreenBlock-thread workgroups
+            constexpr int W = kScreenBlock;
+            const dim3 g((unsigned)((n + W - 1) / W));
+            if (variant == 2)
+                hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, true, W>), g, dim3(W), lds, st, s, a, b, n, rgb, rc,
+                                   sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
+            else if (variant == 1)
+                hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, false, W>), g, dim3(W), lds + slot_bytes(B, true, W),
+                                   st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
+            else
+                hipLaunchKernelGGL((rt_trace_rays_kernel<B, false, false, W>), g, dim3(W), lds + slot_bytes(B, false, W),
+                                   st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
+            return hipGetLastError();
+        }
         if (variant == 2)
             hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, true>), grid, dim3(kThreads), lds, st, s, a, b, n, rgb, rc,
                                sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);

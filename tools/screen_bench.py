@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time the reference-faithful rayTraceScreen: rt_render_screen (GPU chunks) vs the serial C restatement
 (oracle/rt_oracle.c, one core — the frame is a serial chain).  RT_SCREEN_PROFILE=1 prints the phases.
-usage: screen_bench.py [scene W H ...]"""
+usage: screen_bench.py [scene W H ...]        LIB=<path>: another build of librt_amd.so (A/B)"""
 import ctypes
 import json
 import os
@@ -15,12 +15,25 @@ import numpy as np  # noqa: E402
 
 from oracle import pyoracle as po  # noqa: E402
 from ray_tracer_fragment_shader_amd import abi, scenes  # noqa: E402
-from ray_tracer_fragment_shader_amd.tracer import Tracer  # noqa: E402
+
+
+def load_lib():
+    path = os.environ.get("LIB")
+    if not path:
+        return abi.lib()
+    L = ctypes.CDLL(path)
+    for fn, (res, argt) in abi.SIGNATURES.items():
+        if hasattr(L, fn):
+            getattr(L, fn).restype = res
+            getattr(L, fn).argtypes = argt
+    return L
 
 
 def main():
     args = sys.argv[1:] or ["demo", "500", "500", "c2", "640", "360"]
-    tr = Tracer(0)
+    L = load_lib()
+    ctx = ctypes.c_void_p()
+    abi.check(L.rt_ctx_create(0, ctypes.byref(ctx)), "rt_ctx_create")
     for k in range(0, len(args), 3):
         name, W, H = args[k], int(args[k + 1]), int(args[k + 2])
         sc = scenes.CONFIGS[name].scene()
@@ -30,11 +43,11 @@ def main():
         ns = np.zeros((H, W), np.uint8)
         calls = ctypes.c_uint64()
         # warm-up call (first launch of the trace kernel variant, host/device allocations), then timed
-        abi.check(abi.lib().rt_render_screen(tr._ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, 5, 0, 1,
+        abi.check(L.rt_render_screen(ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, 5, 0, 1,
                                              rgb.ctypes.data, None, ns.ctypes.data, ctypes.byref(calls)),
                   "rt_render_screen")
         t = time.perf_counter()
-        abi.check(abi.lib().rt_render_screen(tr._ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, 5, 0, 1,
+        abi.check(L.rt_render_screen(ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, 5, 0, 1,
                                              rgb.ctypes.data, None, ns.ctypes.data, ctypes.byref(calls)),
                   "rt_render_screen")
         t_gpu = time.perf_counter() - t
