@@ -80,8 +80,8 @@ __global__ __launch_bounds__(256) void rt_cone_permute_kernel(const uint64_t* __
                                                               int tiles_y, uint64_t* __restrict__ by_dispatch) {
     const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x, n = (size_t)tiles_x * tiles_y;
     if (k >= n) return;
-    const int gy = (int)(k / tiles_x), tx = (int)(k - (size_t)gy * tiles_x);
-    by_dispatch[cone_slot(k, n)] = by_tile[(size_t)order[gy] * tiles_x + tx];
+    const int gy = (int)(k / tiles_x), bx = (int)(k - (size_t)gy * tiles_x);
+    by_dispatch[cone_slot(k, n)] = by_tile[(size_t)order[gy] * tiles_x + tile_col(bx, gy, tiles_x)];
 }
 
 // Per-eye primary-ray sphere data (run by rt_render_dev when the camera eye changes): deltaP = C - eye

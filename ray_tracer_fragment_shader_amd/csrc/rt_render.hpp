@@ -82,6 +82,27 @@ __host__ __device__ constexpr int slot_bytes(int B, bool transp, int wg = kSlotS
     return (colour_slots(B, transp) * 3 * 8 + (transp ? (B + 1) * 4 : 0)) * wg;
 }
 
+// Image tile column traced at grid column bx of dispatch row gy.  The dispatcher sends workgroup L = gy * tiles_x + bx
+// to XCD L mod 8; with tiles_x a multiple of 8 (every benchmark width) XCD j would trace the same image columns
+// (j mod 8) in every row — a fixed vertical stripe set whose cost depends on the scene (c2: XCDs ending 31.9 to
+// 35.7 us into a 35.7-us launch, wave trace).  RT_XCD_SWIZZLE=1 rotates the columns by gy mod 8, handing each XCD
+// every column class over 8 rows: the XCDs then end within 1.5 us of each other, but c2 runs +1.3% serial, +0.6% in
+// flight (c3, c5 within 0.6%; in-process A/B) — the stripes were not what held the launch's end.  Off.
+#ifndef RT_XCD_SWIZZLE
+#define RT_XCD_SWIZZLE 0
+#endif
+__host__ __device__ __forceinline__ int tile_col(int bx, int gy, int tiles_x) {
+#if RT_XCD_SWIZZLE
+    const int rot = (gy & 7) < tiles_x ? (gy & 7) : 0;
+    const int c = bx + rot;
+    return c >= tiles_x ? c - tiles_x : c;
+#else
+    (void)gy;
+    (void)tiles_x;
+    return bx;
+#endif
+}
+
 // Slot of dispatch position L (linear workgroup id) in the cached cone-mask buffer of n positions: grouped by
 // L mod 8, the XCD the round-robin dispatcher sends workgroup L to (up to a per-launch rotation), so each XCD
 // reads a contiguous run of the buffer and no L2 line is fetched by more than one XCD.
@@ -260,8 +281,9 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     const int bx0 = wave * bw, by0 = 0;
     const int cx = bx0 + (lane & 7);               // column inside the tile
     const int cy = lane >> 3;                      // row inside the tile
-    const int tx = blockIdx.x;                      // 2-D grid: tiles_x x tiles_y
+    const int bxd = blockIdx.x;                     // 2-D grid: tiles_x x tiles_y
     const int gy = (int)(blockIdx.z * kGridY + blockIdx.y);    // tile rows beyond kGridY go to grid.z
+    const int tx = tile_col(bxd, gy, P.tiles_x);    // the image tile column
     // (a const __restrict__ kernel argument: a scalar load, issued beside the other argument loads; through
     // RenderParams it was a vector load the whole prologue waited for)
     // Padding tiles of the last grid.z slice trace a clamped tile and store nothing (no early return: a branch
@@ -272,7 +294,7 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     // without a cache the load reads the scene header instead (a valid address) and the value is unused.
     // (positions past the last tile row — grid.z padding — read the last row's entry: in bounds, unused)
     const int gyc = gy < P.tile_rows_n ? gy : P.tile_rows_n - 1;
-    const uint64_t* cone_p = cone_in ? cone_in + cone_slot((size_t)gyc * P.tiles_x + tx, (size_t)P.tile_rows_n * P.tiles_x)
+    const uint64_t* cone_p = cone_in ? cone_in + cone_slot((size_t)gyc * P.tiles_x + bxd, (size_t)P.tile_rows_n * P.tiles_x)
                                      : reinterpret_cast<const uint64_t*>(gscene);
     const uint64_t cone_cached = *cone_p;
     asm volatile("" ::"s"(cone_cached), "s"(ty_raw));
