@@ -1271,7 +1271,15 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
 #define RT_ACC_LDS_MAX_B 1
 #endif
 __host__ __device__ constexpr bool acc_lds(int B, bool transp) { return !transp && B >= 1 && B <= RT_ACC_LDS_MAX_B; }
-__host__ __device__ constexpr int colour_slots(int B, bool transp) { return B + 1 + (acc_lds(B, transp) ? 1 : 0); }
+// The culling variant keeps its last level's colour in registers (RT_CULL_LAST_REG): B colour slots instead of
+// B + 1, so depth 3 needs 4.5 KB of LDS per one-wave workgroup instead of 6 KB — 35 workgroups per CU instead of
+// 26, i.e. room for a seventh wave per SIMD.
+#ifndef RT_CULL_LAST_REG
+#define RT_CULL_LAST_REG 1
+#endif
+__host__ __device__ constexpr int colour_slots(int B, bool transp, bool cull = false) {
+    return cull && RT_CULL_LAST_REG && !transp ? B : B + 1 + (acc_lds(B, transp) ? 1 : 0);
+}
 
 // rayTraceRay(g_scene, lights, Line(p0, p1), color, B) with color starting at 0 (:1184-1249), as a loop.
 // Every hit of a non-tree scene spawns exactly one continuation (host-checked; ray trees: trace_tree): the
@@ -1328,7 +1336,10 @@ __device__ __forceinline__ void next_ray(d3 p, d3 nd, d3 nu, Ray* r) {
 // shadow_bundle_mask reduce over it).  Returns false when no lane hit (the bounce loop ends).
 template <int B, bool TRANSP, int SS = kSlotStride>
 __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool first, bool alive, uint64_t cone, Ray* r, int* levels,
-                                           double* slot, int* mslot, int* skip, bool lazy_u) {
+                                           double* slot, int* mslot, int* skip, bool lazy_u, d3* last) {
+    // the last level's colour stays in registers (RT_CULL_LAST_REG): slot B does not exist, so the continuation
+    // of level B - 1 parks only its end - start and recomputes its unit direction after the light loop
+    constexpr bool kLastReg = RT_CULL_LAST_REG && !TRANSP;
     uint64_t smask = ~0ull;
     RT_COUNT(V.S, kCntLevels, 1);
     if (!first) {
@@ -1360,13 +1371,15 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
         if (kParkCull && lvl < B) {
             // the continuation (end - start and unit direction) waits in this and the next level's LDS
             // slots across the light loop: no registers, no unit() after it (as in the fast loop)
-            const d3 nu = (TRANSP && V.S->mat[mat].transmit) ? unit(nd) : rdir;
             psl[0] = nd.x;
             psl[SS] = nd.y;
             psl[2 * SS] = nd.z;
-            psl[3 * SS] = nu.x;
-            psl[4 * SS] = nu.y;
-            psl[5 * SS] = nu.z;
+            if (!(kLastReg && lvl == B - 1)) {
+                const d3 nu = (TRANSP && V.S->mat[mat].transmit) ? unit(nd) : rdir;
+                psl[3 * SS] = nu.x;
+                psl[4 * SS] = nu.y;
+                psl[5 * SS] = nu.z;
+            }
             asm volatile("" ::: "memory");
         }
     }
@@ -1376,9 +1389,12 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
         if (kParkCull && lvl < B) {
             asm volatile("" ::: "memory");
             nd = mk(psl[0], psl[SS], psl[2 * SS]);
-            nu = mk(psl[3 * SS], psl[4 * SS], psl[5 * SS]);
+            // (opaque: nd is the reflected ray's end - start, so unit(nd) is rdir, the same operations)
+            if (kLastReg && lvl == B - 1) nu = unit(nd);
+            else nu = mk(psl[3 * SS], psl[4 * SS], psl[5 * SS]);
         }
-        park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
+        if (kLastReg && lvl == B) *last = c;
+        else park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
         *levels = lvl + 1;
     }
     if (lvl < B) {
@@ -1405,6 +1421,8 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t c
     else set_dir(&r, d, unit(d));
     // rays traced (seg, shadow) follow from `levels`: every lane traces levels 0 .. min(levels, B), nl shadow rays per hit
     int skip = -1;                                          // origin_skip of r's origin
+    d3 last = mk(0.0, 0.0, 0.0);                            // CULL, RT_CULL_LAST_REG: level B's colour
+    constexpr bool kLastReg = CULL && RT_CULL_LAST_REG && !TRANSP;
     constexpr bool kSkip = !TRANSP && B >= RT_SKIP_FAST_MIN_B;  // fast loop: origin skips from this depth
     constexpr bool kPark = B >= RT_PARK_ND_MIN_B;
 #if RT_UNROLL_LEVELS
@@ -1418,7 +1436,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t c
         const bool first = PRIMARY && lvl == 0;
         if (CULL) {
             if (!cull_level<B, TRANSP, SS>(V, lvl, first, alive, cone, &r, &levels, slot, mslot,
-                                           &skip, lazy_u))
+                                           &skip, lazy_u, &last))
                 break;
         } else {
             d3 p = mk(0.0, 0.0, 0.0);
@@ -1491,7 +1509,9 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t c
 #pragma unroll 1
     for (int lvl = levels - 1; lvl >= 0; --lvl) {
         const double* sl = slot + 3 * lvl * SS;
-        d3 c = mk(sl[0], sl[SS], sl[2 * SS]);
+        d3 c;
+        if (kLastReg && lvl == B) c = last;             // (RT_CULL_LAST_REG: level B's colour in registers)
+        else c = mk(sl[0], sl[SS], sl[2 * SS]);
         if (lvl == levels - 1) acc = c;
         else acc = TRANSP ? add(c, had(ld3(S->mat[mslot[lvl * SS]].w), acc)) : add(c, acc);
     }

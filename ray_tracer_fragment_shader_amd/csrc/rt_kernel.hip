@@ -839,13 +839,13 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
     } else {
         // >= kConeMin spheres: the wave-culling variant (secondary and shadow rays, rt_device.hpp CULL).
         L.variant = cull ? (mw5 ? kVarCull : kVarCullAnyW) : (mw5 ? kVarFast : kVarFastAnyW);
-        L.lds = slot_bytes(depth, false, RT_WG_FAST);
+        L.lds = slot_bytes(depth, false, RT_WG_FAST, cull);
     }
     if (packed) {                                       // the instances with runtime pixel-format stores
         if (c->tree) L.variant = kVarTreePacked;
         else if (c->transparent) L.variant = kVarTranspPacked;
         else L.variant = cull ? kVarCullPacked : kVarFastPacked;
-        if (!c->tree && !c->transparent) L.lds = slot_bytes(depth, false, RT_WG_FAST);
+        if (!c->tree && !c->transparent) L.lds = slot_bytes(depth, false, RT_WG_FAST, cull);
     }
     switch (depth) {
         case 0: e = launch_render<0>(L); break;

@@ -47,9 +47,20 @@
 #ifndef RT_PIX_RECOMPUTE
 #define RT_PIX_RECOMPUTE 0
 #endif
-#ifndef RT_MINW_CULL
-#define RT_MINW_CULL 5                         // the culling variant (>= kConeMin spheres): 87 VGPRs, no spills
+// ... but in the 7-wave culling kernels it is what keeps the pixel position out of scratch (12 B/lane spilled at
+// the prologue and reloaded for the stores otherwise): on for them.
+#ifndef RT_PIX_RECOMPUTE_CULL
+#define RT_PIX_RECOMPUTE_CULL 1
 #endif
+// The culling variant (>= kConeMin spheres): 7 waves per SIMD (72 VGPRs, 94 SGPRs with 30 spilled to VGPR lanes,
+// 12 B/lane of scratch), which its LDS allows since the last level's colour stays in registers (RT_CULL_LAST_REG:
+// 4.5 KB per workgroup at depth 3).  c5 -2.6% serial, -3.9% with 3 frames in flight against the same code at 6
+// waves (77 VGPRs, no scratch; in-process A/B).
+#ifndef RT_MINW_CULL
+#define RT_MINW_CULL 7
+#endif
+// (depth 2 spills 12 B/lane at 7 waves even with the store position recomputed: 6 waves there, 75 VGPRs, no scratch)
+__host__ __device__ constexpr int cull_min_waves(int B) { return B == 2 && RT_MINW_CULL > 6 ? 6 : RT_MINW_CULL; }
 // Default launch-bound waves per SIMD of the fast kernels by depth: 6 up to depth 2, 5 from depth 3.  The bound
 // is a floor: the depth 1 and 2 kernels come out at 63 / 67 VGPRs under it (8 / 7 waves by VGPRs; the c2 kernel
 // accumulates its colour in LDS, shade ACC) and their SGPR cap (rt_render_kernel_sg, 96) gives them 7 waves per
@@ -78,8 +89,8 @@ constexpr int kFmt8_RGBA = 0, kFmt8_RGB = 1, kFmt8_GRAY = 2;  // byte image
 // LDS bytes of trace()'s per-level slots for depth B: 3 doubles per colour slot (colour_slots: one per level,
 // plus one for the parked continuation when the colour accumulates in LDS) and the material id per level when
 // TRANSP, per work-item of a `wg`-thread workgroup.
-__host__ __device__ constexpr int slot_bytes(int B, bool transp, int wg = kSlotStride) {
-    return (colour_slots(B, transp) * 3 * 8 + (transp ? (B + 1) * 4 : 0)) * wg;
+__host__ __device__ constexpr int slot_bytes(int B, bool transp, int wg = kSlotStride, bool cull = false) {
+    return (colour_slots(B, transp, cull) * 3 * 8 + (transp ? (B + 1) * 4 : 0)) * wg;
 }
 
 // Image tile column traced at grid column bx of dispatch row gy.  The dispatcher sends workgroup L = gy * tiles_x + bx
@@ -261,8 +272,8 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
         off = P.lds_bytes;
     }
     double* slot = reinterpret_cast<double*>(smem + off) + tid;
-    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * colour_slots(B, TRANSP) * WG) + tid;
-    off += slot_bytes(B, TRANSP, WG);
+    int* mslot = reinterpret_cast<int*>(smem + off + 3 * 8 * colour_slots(B, TRANSP, CULL) * WG) + tid;
+    off += slot_bytes(B, TRANSP, WG, CULL);
     float4* st32 = reinterpret_cast<float4*>(smem + off);                              // [8][32] 4 KB
     double* st64 = reinterpret_cast<double*>(smem + off + 4096);                        // [8][32][3] 6 KB
     uint32_t* strc = reinterpret_cast<uint32_t*>(smem + off + 4096 + 6144);             // [8][32] 1 KB
@@ -361,6 +372,8 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
         int tid_e = tid;
 #if RT_PIX_RECOMPUTE
         asm volatile("" : "+v"(tid_e));
+#else
+        if constexpr (CULL && RT_PIX_RECOMPUTE_CULL) asm volatile("" : "+v"(tid_e));
 #endif
         const int lane_e = tid_e & 63;
         const int i_e = tx * TW + (tid_e >> 6) * bw + (lane_e & 7), lr_e = ty_st * kTileH + (lane_e >> 3);
@@ -601,7 +614,7 @@ hipError_t launch_render_impl(const RenderLaunch& L) {
                 if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return launch_render_sg<B, MW, false>(L);
                 return launch_render_one<B, 0, MW, false, false, RT_WG_FAST, false>(L);
             case kVarFastAnyW: return launch_render_one<B, 0, 1, false, false, RT_WG_FAST, false>(L);
-            case kVarCull: return launch_render_one<B, 0, RT_MINW_CULL, false, true, RT_WG_FAST, false>(L);
+            case kVarCull: return launch_render_one<B, 0, cull_min_waves(B), false, true, RT_WG_FAST, false>(L);
             case kVarCullAnyW: return launch_render_one<B, 0, 1, false, true, RT_WG_FAST, false>(L);
             case kVarTransp: return launch_render_one<B, 0, 1, true, false, 64, false>(L);
             case kVarTree: return launch_render_one<B, 0, 1, true, false, 64, true>(L);
@@ -612,7 +625,7 @@ hipError_t launch_render_impl(const RenderLaunch& L) {
                 if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return launch_render_sg<B, MW, true>(L);
                 return launch_render_one<B, 0, (B <= 3 ? MW : 1), false, false, RT_WG_FAST, false, true>(L);
             case kVarCullPacked:
-                return launch_render_one<B, 0, (B <= 3 ? RT_MINW_CULL : 1), false, true, RT_WG_FAST, false, true>(L);
+                return launch_render_one<B, 0, (B <= 3 ? cull_min_waves(B) : 1), false, true, RT_WG_FAST, false, true>(L);
             case kVarTranspPacked: return launch_render_one<B, 0, 1, true, false, 64, false, true>(L);
             case kVarTreePacked: return launch_render_one<B, 0, 1, true, false, 64, true, true>(L);
             default: return hipErrorInvalidValue;
@@ -660,7 +673,7 @@ const void* render_kernel_ptr_impl(int variant) {
         return nullptr;
     } else {
         constexpr int kFast = B <= 3 ? (RT_MINW != 0 ? RT_MINW : kDefaultMinWaves(B)) : 1;
-        constexpr int kCull = B <= 3 ? RT_MINW_CULL : 1;
+        constexpr int kCull = B <= 3 ? cull_min_waves(B) : 1;
         switch (variant) {
             case 0:
                 if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return (const void*)rt_render_kernel_sg<B, kFast, false, false>;

@@ -692,9 +692,9 @@ def test_origin_skips_edge_cases(tr):
 
 def test_render_kernels_do_not_spill(tr):
     """The render kernels the benchmark configs launch keep everything in registers (private scratch would
-    be written back to HBM: PMC showed 1.2x the algorithmic write bytes when the bounce loop spilled), and
-    the depth <= 2 fast kernels fit 6 waves per SIMD (<= 80 VGPRs).  rt_diag_kernel_resources reads the
-    instances' hipFuncGetAttributes."""
+    be written back to HBM: PMC showed 1.2x the algorithmic write bytes when the r02 bounce loop spilled 36 B/lane),
+    and the depth <= 2 fast kernels fit 6 waves per SIMD (<= 80 VGPRs), the culling kernels of depth 0, 1 and 3
+    seven (<= 72 VGPRs, r04).  rt_diag_kernel_resources reads the instances' hipFuncGetAttributes."""
     L = abi.lib()
     regs, scratch = ctypes.c_int(), ctypes.c_int()
     table = {}
@@ -707,6 +707,8 @@ def test_render_kernels_do_not_spill(tr):
     for depth in range(4):                           # c1..c5: spheres + board, and the culling variant
         assert table[(0, depth)][1] == 0, (depth, table[(0, depth)])
         assert table[(1, depth)][1] == 0, (depth, table[(1, depth)])
+        if depth != 2:
+            assert table[(1, depth)][0] <= 72, (depth, table[(1, depth)])   # 7 waves per SIMD
     for depth in range(3):
         assert table[(0, depth)][0] <= 80, (depth, table[(0, depth)])
     assert table[(3, 3)][1] > 0                     # the ray-tree node stack lives in scratch by design
