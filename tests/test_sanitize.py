@@ -13,11 +13,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SAN = os.path.join(ROOT, "tests", "sanitize")
 
 
+# rt_render_screen's pipeline depths: the default (one continuation queued behind the chunk being resolved), two
+# continuations (RT_SCREEN_AHEAD=2: several dropped at once, buffer sets drained out of order) and none
+# (RT_SCREEN_NEXT=0: r03's one chunk in flight).
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
-def test_host_code_under_asan_ubsan(tmp_path):
+@pytest.mark.parametrize("screen_env", [{}, {"RT_SCREEN_AHEAD": "2"}, {"RT_SCREEN_NEXT": "0"}],
+                         ids=["default", "ahead2", "next0"])
+def test_host_code_under_asan_ubsan(tmp_path, screen_env):
     r = subprocess.run(["make", "-C", SAN, "-j8"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0", UBSAN_OPTIONS="print_stacktrace=1")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0", UBSAN_OPTIONS="print_stacktrace=1",
+               **screen_env)
     r = subprocess.run([os.path.join(SAN, "_build", "san_main")], capture_output=True, text=True, timeout=600,
                        cwd=tmp_path, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
