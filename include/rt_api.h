@@ -258,9 +258,12 @@ int rt_host_free(void* p);
  * right and up'), every sample jittered by 0.5 * randomUnit() (:1148-1169, rand() arguments evaluated
  * right to left), up to 16 samples per pixel with the reference's convergence test (:1294-1311), and the
  * average colour carried from pixel to pixel (:1283).  The carry-over and the shared rand() stream make
- * the frame a serial chain; the samples are traced on the GPU in speculative chunks (the sample count of
- * each pixel is predicted, the host resolves the chain in order and re-issues the chunk after the first
- * wrong prediction), so the result is the reference's, bit for bit.
+ * the frame a serial chain; the samples are traced on the GPU in speculative chunks (each pixel's sample
+ * count is predicted and a window of stream positions around the prediction is traced; the host resolves the
+ * chain in order, with the continuation of the chain already queued, and restarts it where the actual stream
+ * position leaves a window), so the result is the reference's, bit for bit.  The context keeps the chunks'
+ * buffers between calls (≈ 40 MB of mapped host memory and three streams, freed by rt_ctx_destroy); concurrent
+ * calls on one context are allowed (each beyond the first allocates its own).
  * rand_kind: RT_RAND_GLIBC (glibc rand(), the reference built on Linux) or RT_RAND_MSVC (the MSVC CRT
  * LCG, the reference's own Visual Studio build); seed as given to srand (the app never calls srand: 1).
  * Host outputs, each nullable, width*height pixels, j = 0 bottom: rgb64f (the colour passed to
