@@ -262,8 +262,9 @@ int rt_host_free(void* p);
  * count is predicted and a window of stream positions around the prediction is traced; the host resolves the
  * chain in order, with the continuation of the chain already queued, and restarts it where the actual stream
  * position leaves a window), so the result is the reference's, bit for bit.  The context keeps the chunks'
- * buffers between calls (≈ 40 MB of mapped host memory and three streams, freed by rt_ctx_destroy); concurrent
- * calls on one context are allowed (each beyond the first allocates its own).
+ * buffers between calls (≈ 14 MB of mapped host memory and a stream per buffer set, three sets in the default
+ * pipeline; freed by rt_ctx_destroy); concurrent calls on one context are allowed (each beyond the first
+ * allocates its own).
  * rand_kind: RT_RAND_GLIBC (glibc rand(), the reference built on Linux) or RT_RAND_MSVC (the MSVC CRT
  * LCG, the reference's own Visual Studio build); seed as given to srand (the app never calls srand: 1).
  * Host outputs, each nullable, width*height pixels, j = 0 bottom: rgb64f (the colour passed to

@@ -201,23 +201,29 @@ struct ScreenWs {                                                    // chunks i
 constexpr size_t kPixBytes = (size_t)kScreenMaxPix * sizeof(ScreenPix);
 constexpr size_t kPixTableBytes = kPixBytes + (size_t)kScreenMaxBlocks * sizeof(int32_t);
 
+// A buffer set's stream, event and mapped buffers, allocated on the set's first use (the default pipeline uses
+// three of the kSets).
+hipError_t alloc_set(ScreenBuf& b) {
+    const size_t ray_bytes = (size_t)kScreenMaxRays * 3 * sizeof(double);
+    const unsigned mapped = hipHostMallocMapped | hipHostMallocCoherent;
+    hipError_t e = hipSuccess;                                       // (a set left half-built by a failure resumes)
+    if (!b.st.s) e = hipStreamCreateWithFlags(&b.st.s, hipStreamNonBlocking);
+    b.sp.resize(3 * (size_t)kScreenMaxPix);
+    if (e == hipSuccess && !b.h_rgb.p) e = hipHostMalloc(&b.h_rgb.p, ray_bytes, mapped);
+    if (e == hipSuccess && !b.h_pix.p) e = hipHostMalloc(&b.h_pix.p, kPixTableBytes, mapped);
+    if (e == hipSuccess && !b.h_jit.p) e = hipHostMalloc(&b.h_jit.p, (size_t)kScreenMaxJit * 3 * sizeof(double), mapped);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_rgb, b.h_rgb.p, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_pix, b.h_pix.p, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_jit, b.h_jit.p, 0);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
+    return e;
+}
+
 std::unique_ptr<ScreenWs> alloc_ws() {
     std::unique_ptr<ScreenWs> w(new ScreenWs());
-    const size_t ray_bytes = (size_t)kScreenMaxRays * 3 * sizeof(double);
     const unsigned mapped = hipHostMallocMapped | hipHostMallocCoherent;
     hipError_t e = hipHostMalloc(&w->h_cam.p, 3 * sizeof(double), mapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer(&w->d_cam, w->h_cam.p, 0);
-    for (ScreenBuf& b : w->buf) {
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&b.st.s, hipStreamNonBlocking);
-        b.sp.resize(3 * (size_t)kScreenMaxPix);
-        if (e == hipSuccess) e = hipHostMalloc(&b.h_rgb.p, ray_bytes, mapped);
-        if (e == hipSuccess) e = hipHostMalloc(&b.h_pix.p, kPixTableBytes, mapped);
-        if (e == hipSuccess) e = hipHostMalloc(&b.h_jit.p, (size_t)kScreenMaxJit * 3 * sizeof(double), mapped);
-        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_rgb, b.h_rgb.p, 0);
-        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_pix, b.h_pix.p, 0);
-        if (e == hipSuccess) e = hipHostGetDevicePointer(&b.d_jit, b.h_jit.p, 0);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
-    }
     if (e != hipSuccess) return nullptr;
     return w;
 }
@@ -309,7 +315,8 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         rt_ctx* ctx;                                                 // done, then the workspace goes back
         std::unique_ptr<ScreenWs>& ws;
         ~Give() {
-            for (ScreenBuf& b : ws->buf) (void)hipStreamSynchronize(b.st.s);
+            for (ScreenBuf& b : ws->buf)
+                if (b.st.s) (void)hipStreamSynchronize(b.st.s);
             give_ws(ctx, std::move(ws));
         }
     } give{ctx, ws};
@@ -336,6 +343,13 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     int ahead = 1;
     if (const char* ev = getenv("RT_SCREEN_AHEAD")) ahead = atoi(ev);
     ahead = next_mul > 0 ? std::min(std::max(ahead, 1), ScreenWs::kAheadMax) : 0;
+    // RT_SCREEN_NEXT_MIN: continuations only once the chunk size has grown to at least this many pixels (a run of
+    // clean chunks); after a break the chain waits for each chunk before queueing the next.  Two thirds of the
+    // continuations queued behind every chunk were dropped (583 of 886 on the demo frame), and their building and
+    // tracing cost more than they saved: in-process A/B (tools/screen_ab.py), against none at all, demo -9%,
+    // c2 scene -6% with continuations from the maximum chunk size (4,096 pixels) on; from 0 pixels +1–3%.
+    int next_min = kMaxPix;
+    if (const char* ev = getenv("RT_SCREEN_NEXT_MIN")) next_min = std::max(0, atoi(ev));
     using clk = std::chrono::steady_clock;
     double t_build = 0, t_gen = 0, t_gpu = 0, t_res = 0;
     const auto t_start = clk::now();
@@ -415,9 +429,13 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // their own streams while the chain goes on in the other sets).
     bool in_use[ScreenWs::kSets] = {};
     auto pick = [&](int* out) -> int {
-        int idle = -1;
+        int idle = -1, fresh = -1;
         for (int b = 0; b < ScreenWs::kSets; ++b) {
             if (in_use[b]) continue;
+            if (!buf[b].done) {                                  // never used
+                if (fresh < 0) fresh = b;
+                continue;
+            }
             const hipError_t q = hipEventQuery(buf[b].done);
             if (q == hipSuccess) {
                 *out = b;
@@ -426,12 +444,17 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
             if (q != hipErrorNotReady) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(q));
             if (idle < 0) idle = b;
         }
+        if (fresh >= 0) {
+            const hipError_t q = alloc_set(buf[fresh]);
+            if (q != hipSuccess) return rt_fail(RT_ENOMEM, std::string("rt_render_screen: ") + hipGetErrorString(q));
+            *out = fresh;
+            return RT_OK;
+        }
         const hipError_t q = hipEventSynchronize(buf[idle].done);   // (kSets > 1 + kAheadMax: one exists)
         if (q != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_screen: ") + hipGetErrorString(q));
         *out = idle;
         return RT_OK;
-    };
-    auto queue_in_free = [&](std::deque<Chunk>& fl, long long p0, uint64_t pred_start, uint64_t floor, V3 w0,
+    };    auto queue_in_free = [&](std::deque<Chunk>& fl, long long p0, uint64_t pred_start, uint64_t floor, V3 w0,
                              int want) -> int {
         int b = 0;
         int r = pick(&b);
@@ -447,7 +470,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     if ((rc = queue_in_free(fl, 0, 0, 0, walk, chunk))) return rc;
     while (p < P) {
         // continuations of the prediction chain, queued behind the chunk about to be resolved
-        while ((int)fl.size() < 1 + ahead && fl.back().p0 + fl.back().m < P) {
+        while ((int)fl.size() < 1 + ahead && chunk >= next_min && fl.back().p0 + fl.back().m < P) {
             const Chunk t = fl.back();
             if ((rc = queue_in_free(fl, t.p0 + t.m, t.S0 + (uint64_t)t.spred_end, S, t.walk_end,
                                     std::min(chunk * next_mul, kMaxPix))))

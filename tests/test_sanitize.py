@@ -13,12 +13,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SAN = os.path.join(ROOT, "tests", "sanitize")
 
 
-# rt_render_screen's pipeline depths: the default (one continuation queued behind the chunk being resolved), two
-# continuations (RT_SCREEN_AHEAD=2: several dropped at once, buffer sets drained out of order) and none
-# (RT_SCREEN_NEXT=0: r03's one chunk in flight).
+# rt_render_screen's pipelines: the default (a continuation only behind maximum-size chunks, which these small
+# frames never reach), a continuation behind every chunk (RT_SCREEN_NEXT_MIN=0: many dropped), two of them
+# (RT_SCREEN_AHEAD=2: several dropped at once, buffer sets drained out of order) and none (RT_SCREEN_NEXT=0).
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
-@pytest.mark.parametrize("screen_env", [{}, {"RT_SCREEN_AHEAD": "2"}, {"RT_SCREEN_NEXT": "0"}],
-                         ids=["default", "ahead2", "next0"])
+@pytest.mark.parametrize("screen_env", [{}, {"RT_SCREEN_NEXT_MIN": "0"},
+                                        {"RT_SCREEN_NEXT_MIN": "0", "RT_SCREEN_AHEAD": "2"}, {"RT_SCREEN_NEXT": "0"}],
+                         ids=["default", "every_chunk", "ahead2", "next0"])
 def test_host_code_under_asan_ubsan(tmp_path, screen_env):
     r = subprocess.run(["make", "-C", SAN, "-j8"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
