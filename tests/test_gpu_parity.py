@@ -473,6 +473,21 @@ def test_render_screen_faithful_vs_oracle(tr, name, W, H, rng, seed):
             assert calls == g["calls"]
 
 
+@pytest.mark.parametrize("env", [{"RT_SCREEN_NEXT_MIN": "0"}, {"RT_SCREEN_NEXT_MIN": "0", "RT_SCREEN_AHEAD": "2"},
+                                 {"RT_SCREEN_NEXT": "0"}], ids=["every_chunk", "ahead2", "next0"])
+def test_render_screen_pipelines_vs_oracle(tr, monkeypatch, env):
+    """The chunk pipelines the default rarely takes on small frames (continuations behind every chunk, two of them,
+    none), read from the environment at each call: the same frame, bit for bit, as the serial restatement."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sc = scenes.CONFIGS["demo"].scene()
+    for rng, seed, W, H in ((0, 1, 160, 120), (1, 4, 97, 61)):
+        rgb, _, ns, calls = _render_screen(tr, sc, W, H, 5, rng, seed)
+        want_rgb, want_ns, want_calls = po.render_screen(sc.to_abi(), W, H, 5, rng, seed)
+        assert np.array_equal(ns, want_ns) and calls == want_calls
+        assert np.array_equal(rgb, want_rgb)
+
+
 def test_cli_faithful_screen_ppm(tmp_path):
     """`rt_render --config demo --faithful msvc`: the app's rayTraceScreen frame through rt_render_screen."""
     import subprocess
