@@ -373,7 +373,8 @@ def dropin_binding_legs(W, H, B, cfg, frames=30):
             except Exception as exc:                        # reported, the timed metric stands
                 res[name] = {"error": f"{type(exc).__name__}: {exc}"}
     res["note"] = (f"lib/rt_dropin --frames {frames} (the committed INTEGRATION.md binding, C++, built against "
-                   "rt_api.h): its own steady-state ms per draw() after the first frame, host to host")
+                   "rt_api.h): its own steady-state ms per draw() after the first three frames (scene upload, first render, "
+                   "calibration render), host to host")
     return res
 
 

@@ -160,14 +160,17 @@ int main(int argc, char** argv) {
    }
    try {
       loadScene(format);
-      draw();                                           // first frame: scene upload, first render of the view
+      // the first frames: scene upload and first render of the view, then the calibration render that times its tile
+      // rows (rt_render_dev's adaptive order) — not the steady state the SDL loop repeats
+      const int warm = frames > 3 ? 3 : 1;
+      for (int k = 0; k < warm; ++k) draw();
       const auto t0 = chrono::steady_clock::now();
-      for (int k = 1; k < frames; ++k) draw();          // steady state: what the SDL loop repeats per frame
-      const double ms = frames > 1 ? chrono::duration<double, milli>(chrono::steady_clock::now() - t0).count() /
-                                         (frames - 1) : 0.0;
+      for (int k = warm; k < frames; ++k) draw();      // steady state: what the SDL loop repeats per frame
+      const double ms = frames > warm ? chrono::duration<double, milli>(chrono::steady_clock::now() - t0).count() /
+                                            (frames - warm) : 0.0;
       writePpmScreenshot(g_windowWidth, g_windowHeight, out.c_str());
-      printf("rt_dropin: %dx%d, %d frame(s), %.3f ms per draw() after the first, format %s (%d B/px), %s%s -> %s\n",
-             g_windowWidth, g_windowHeight, frames, ms,
+      printf("rt_dropin: %dx%d, %d frame(s), %.3f ms per draw() after the first %d, format %s (%d B/px), %s%s -> %s\n",
+             g_windowWidth, g_windowHeight, frames, ms, warm,
              g_format == RT_PIXEL_GRAY8 ? "GRAY8" : g_format == RT_PIXEL_RGB8 ? "RGB8" : "RGBA8", g_channels,
              g_pinned ? "pinned" : "pageable", g_pipelined ? ", pipelined" : "", out.c_str());
    } catch (const exception& e) {
