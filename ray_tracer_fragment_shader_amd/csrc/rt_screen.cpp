@@ -348,7 +348,11 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // continuations queued behind every chunk were dropped (583 of 886 on the demo frame), and their building and
     // tracing cost more than they saved: in-process A/B (tools/screen_ab.py), against none at all, demo -9%,
     // c2 scene -6% with continuations from the maximum chunk size (4,096 pixels) on; from 0 pixels +1–3%.
-    int next_min = kMaxPix;
+    // RT_SCREEN_MAX_CHUNK (A/B): the largest chunk (pixels); a chunk is waited for whole before it is resolved.
+    // (Smaller caps, with continuations from the cap on, measured slower: 2,048 ±1%, 1,024 +2–3%, 512 +5–12%.)
+    int max_chunk = kMaxPix;
+    if (const char* ev = getenv("RT_SCREEN_MAX_CHUNK")) max_chunk = std::min(std::max(16, atoi(ev)), kMaxPix);
+    int next_min = max_chunk;
     if (const char* ev = getenv("RT_SCREEN_NEXT_MIN")) next_min = std::max(0, atoi(ev));
     using clk = std::chrono::steady_clock;
     double t_build = 0, t_gen = 0, t_gpu = 0, t_res = 0;
@@ -473,7 +477,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         while ((int)fl.size() < 1 + ahead && chunk >= next_min && fl.back().p0 + fl.back().m < P) {
             const Chunk t = fl.back();
             if ((rc = queue_in_free(fl, t.p0 + t.m, t.S0 + (uint64_t)t.spred_end, S, t.walk_end,
-                                    std::min(chunk * next_mul, kMaxPix))))
+                                    std::min(chunk * next_mul, max_chunk))))
                 return rc;
         }
         // While the GPU traces: generate the stream values the following chunk will need (rand() + normalize
@@ -544,7 +548,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         in_use[cur.b] = false;
         fl.pop_front();
         if (!broke && q == cur.m) {
-            chunk = std::min(kMaxPix, chunk * 2);
+            chunk = std::min(max_chunk, chunk * 2);
             if (fl.empty() && p < P && (rc = queue_in_free(fl, p, S, S, walk, chunk))) return rc;
             continue;
         }
