@@ -44,8 +44,11 @@ int rt_unpack_dev_ex(const void* gathered, const void* rank0_slab, void* image, 
 // (pix[q].off <= k < pix[q].off + pix[q].len), is Line(cam, pix[q].sp + 0.5 * jit[pix[q].base + j])
 // (ray.set(camera, screenPt + .5 * randomUnit()), MSA:1296); first[b] = the pixel of ray b * kScreenBlock.
 // All pointers device-visible; n rays, m pixels.
+// done (nullable, device-visible, one word per workgroup of kScreenBlock rays): each workgroup stores `seq` into its
+// word after its colours are visible system-wide, so the host can resolve a chunk while it is still being traced.
 int rt_trace_screen_dev(rt_ctx* c, const double cam[3], const ScreenPix* pix, const int32_t* first, int m,
-                        const double* jit, int n, int depth, double* rgb64f, void* stream);
+                        const double* jit, int n, int depth, double* rgb64f, uint32_t* done, uint32_t seq,
+                        void* stream);
 constexpr int kScreenMaxRays = 1 << 19;        // rays of one chunk
 constexpr int kScreenMaxPix = 4096;            // pixels of one chunk
 constexpr int kScreenMaxJit = kScreenMaxPix * 16 + 128;   // stream values of one chunk

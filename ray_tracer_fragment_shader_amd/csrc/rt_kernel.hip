@@ -1154,12 +1154,13 @@ extern "C" int rt_trace_rays_dev(rt_ctx* c, const double* starts, const double* 
 }
 
 int rt_trace_screen_dev(rt_ctx* c, const double cam[3], const ScreenPix* pix, const int32_t* first, int m,
-                        const double* jit, int n, int depth, double* rgb64f, void* stream) {
+                        const double* jit, int n, int depth, double* rgb64f, uint32_t* done, uint32_t seq,
+                        void* stream) {
     if (!c || !c->scene_set) return rt_fail(RT_EINVAL, "rt_trace_screen_dev: no context/scene");
     if (depth < 0 || depth > RT_MAX_DEPTH) return rt_fail(RT_EINVAL, "rt_trace_screen_dev: depth out of range");
     if (n <= 0 || m <= 0) return RT_OK;
     ScreenArgs sa;
-    sa.pix = pix, sa.m = m, sa.first = first, sa.jit = jit;
+    sa.pix = pix, sa.m = m, sa.first = first, sa.jit = jit, sa.done = done, sa.seq = seq;
     // RT_SCREEN_LDS=0 (A/B): the scene record read from global memory instead of LDS
     static const bool lds = !getenv("RT_SCREEN_LDS") || atoi(getenv("RT_SCREEN_LDS")) != 0;
     const size_t slots = c->tree ? 0 : slot_bytes(depth, c->transparent, kScreenBlock);

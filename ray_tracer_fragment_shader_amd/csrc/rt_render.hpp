@@ -472,7 +472,8 @@ __global__ __launch_bounds__(WG) void rt_trace_rays_kernel(const DevScene* __res
                                                                  uint32_t* __restrict__ rc,
                                                                  const ScreenPix* __restrict__ spix, int sm,
                                                                  const int32_t* __restrict__ sfirst,
-                                                                 const double* __restrict__ sjit, int scene_lds) {
+                                                                 const double* __restrict__ sjit, int scene_lds,
+                                                                 uint32_t* __restrict__ sdone, uint32_t sseq) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // Every lane traces (trace() reduces over the wave); lanes past n repeat ray n - 1 and store nothing.
     const int k = blockIdx.x * WG + threadIdx.x, kk = k < n ? k : n - 1;
@@ -510,9 +511,15 @@ __global__ __launch_bounds__(WG) void rt_trace_rays_kernel(const DevScene* __res
         c = trace_tree<B>(V, p0, p1, &seg, &sh);
     else
         c = trace<B, false, TRANSP, false, WG>(V, p0, p1, ~0ull, &seg, &sh, slot, mslot);
-    if (k >= n) return;
-    if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
-    if (rc) rc[k] = seg | (sh << 16);
+    if (k < n) {
+        if (rgb) { rgb[3 * k] = c.x; rgb[3 * k + 1] = c.y; rgb[3 * k + 2] = c.z; }
+        if (rc) rc[k] = seg | (sh << 16);
+    }
+    if (sdone) {                                        // screen chunks: this workgroup's colours are out
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(sdone + blockIdx.x, sseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // The screen-mode arguments of a trace launch (all null: a plain ray list).
@@ -522,6 +529,8 @@ struct ScreenArgs {
     const int32_t* first = nullptr;
     const double* jit = nullptr;
     int scene_lds = 0;                 // bytes of the scene record copied into LDS (multiple of 4; 0: none)
+    uint32_t* done = nullptr;          // per-workgroup completion words (rt_trace_screen_dev)
+    uint32_t seq = 0;
 };
 
 // Render-kernel variants rt_render_dev chooses between (rt_kernel.hip).
@@ -645,24 +654,24 @@ hipError_t launch_trace_rays_impl(int variant, dim3 grid, hipStream_t st, const 
             const dim3 g((unsigned)((n + W - 1) / W));
             if (variant == 2)
                 hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, true, W>), g, dim3(W), lds, st, s, a, b, n, rgb, rc,
-                                   sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
+                                   sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds, sa.done, sa.seq);
             else if (variant == 1)
                 hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, false, W>), g, dim3(W), lds + slot_bytes(B, true, W),
-                                   st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
+                                   st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds, sa.done, sa.seq);
             else
                 hipLaunchKernelGGL((rt_trace_rays_kernel<B, false, false, W>), g, dim3(W), lds + slot_bytes(B, false, W),
-                                   st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
+                                   st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds, sa.done, sa.seq);
             return hipGetLastError();
         }
         if (variant == 2)
             hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, true>), grid, dim3(kThreads), lds, st, s, a, b, n, rgb, rc,
-                               sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
+                               sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds, sa.done, sa.seq);
         else if (variant == 1)
             hipLaunchKernelGGL((rt_trace_rays_kernel<B, true, false>), grid, dim3(kThreads), lds + slot_bytes(B, true),
-                               st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
+                               st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds, sa.done, sa.seq);
         else
             hipLaunchKernelGGL((rt_trace_rays_kernel<B, false, false>), grid, dim3(kThreads), lds + slot_bytes(B, false),
-                               st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds);
+                               st, s, a, b, n, rgb, rc, sa.pix, sa.m, sa.first, sa.jit, sa.scene_lds, sa.done, sa.seq);
         return hipGetLastError();
     }
 }

@@ -102,7 +102,7 @@ extern "C" int rt_trace_rays_dev(rt_ctx* c, const double* starts, const double* 
 }
 // rt_render_screen's device-side ray formation (rt_kernel.hip), restated on the host with the same operations.
 int rt_trace_screen_dev(rt_ctx* c, const double cam[3], const ScreenPix* pix, const int32_t* first, int m,
-                        const double* jit, int n, int depth, double* rgb64f, void*) {
+                        const double* jit, int n, int depth, double* rgb64f, uint32_t* done, uint32_t seq, void*) {
     if (!c) return rt_fail(RT_EINVAL, "rt_trace_screen_dev: null context");
     if (n <= 0 || m <= 0) return RT_OK;
     std::vector<double> starts(3 * (size_t)n), ends(3 * (size_t)n);
@@ -121,5 +121,8 @@ int rt_trace_screen_dev(rt_ctx* c, const double cam[3], const ScreenPix* pix, co
         }
     }
     const char* th = getenv("SAN_TRACE_THREADS");
-    return oracle_trace_rays(&c->scene, starts.data(), ends.data(), n, depth, rgb64f, nullptr, th ? atoi(th) : 1);
+    const int rc = oracle_trace_rays(&c->scene, starts.data(), ends.data(), n, depth, rgb64f, nullptr, th ? atoi(th) : 1);
+    if (!rc && done)                                          // every workgroup's done word, after its colours
+        for (int w = 0; w < (n + kScreenBlock - 1) / kScreenBlock; ++w) done[w] = seq;
+    return rc;
 }

@@ -474,7 +474,8 @@ def test_render_screen_faithful_vs_oracle(tr, name, W, H, rng, seed):
 
 
 @pytest.mark.parametrize("env", [{"RT_SCREEN_NEXT_MIN": "0"}, {"RT_SCREEN_NEXT_MIN": "0", "RT_SCREEN_AHEAD": "2"},
-                                 {"RT_SCREEN_NEXT": "0"}], ids=["every_chunk", "ahead2", "next0"])
+                                 {"RT_SCREEN_NEXT": "0"}, {"RT_SCREEN_NEXT_MIN": "0", "RT_SCREEN_PROGRESSIVE": "1"}],
+                         ids=["every_chunk", "ahead2", "next0", "progressive"])
 def test_render_screen_pipelines_vs_oracle(tr, monkeypatch, env):
     """The chunk pipelines the default rarely takes on small frames (continuations behind every chunk, two of them,
     none), read from the environment at each call: the same frame, bit for bit, as the serial restatement."""

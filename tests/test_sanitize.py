@@ -18,8 +18,9 @@ SAN = os.path.join(ROOT, "tests", "sanitize")
 # (RT_SCREEN_AHEAD=2: several dropped at once, buffer sets drained out of order) and none (RT_SCREEN_NEXT=0).
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
 @pytest.mark.parametrize("screen_env", [{}, {"RT_SCREEN_NEXT_MIN": "0"},
-                                        {"RT_SCREEN_NEXT_MIN": "0", "RT_SCREEN_AHEAD": "2"}, {"RT_SCREEN_NEXT": "0"}],
-                         ids=["default", "every_chunk", "ahead2", "next0"])
+                                        {"RT_SCREEN_NEXT_MIN": "0", "RT_SCREEN_AHEAD": "2"}, {"RT_SCREEN_NEXT": "0"},
+                                        {"RT_SCREEN_NEXT_MIN": "0", "RT_SCREEN_PROGRESSIVE": "1"}],
+                         ids=["default", "every_chunk", "ahead2", "next0", "progressive"])
 def test_host_code_under_asan_ubsan(tmp_path, screen_env):
     r = subprocess.run(["make", "-C", SAN, "-j8"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
