@@ -278,9 +278,11 @@ def pipelined_frames(torch, L, abi, trs, sts, launch_args, steps, settle_s):
     ev0 = torch.cuda.Event(enable_timing=True)
     ends = [torch.cuda.Event(enable_timing=True) for _ in sts]
     # The interval's events: a start stamp on the first stream and an end stamp on every stream, compared afterwards
-    # (no cross-stream waits inside the timed region: they only delayed its first launch and its end).
-    t0 = time.perf_counter()
+    # (no cross-stream waits inside the timed region: they only delayed its first launch and its end).  The start
+    # stamp is recorded just before the timer starts (the GPU is idle: it lands at once), so the timed region holds
+    # the frames' launches, their execution and the final synchronisation only.
     ev0.record(s0)
+    t0 = time.perf_counter()
     for i in range(steps):
         rc = fn(*launch_args[i % n])
         if rc:
