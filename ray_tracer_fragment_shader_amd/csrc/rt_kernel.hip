@@ -940,13 +940,25 @@ static void* pinned_device_ptr(const void* host, size_t bytes) {
     return (void*)(it->second.second + (h - it->first));
 }
 
+// The device address of any page-locked host buffer (rt_host_alloc's, or one the caller pinned elsewhere, e.g. a
+// torch pin_memory() tensor): the runtime's pointer attributes; nullptr for pageable memory.
+static void* host_device_ptr(const void* host, size_t bytes) {
+    if (void* d = pinned_device_ptr(host, bytes)) return d;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, host) != hipSuccess) {
+        (void)hipGetLastError();                                     // pageable: not an error of this call
+        return nullptr;
+    }
+    return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
+}
+
 constexpr unsigned kCopyStreamBlocks = 16;     // copy kernel beside a render: workgroups (rt_ctx::copy_mode)
 
 // A copy kernel into rt_host_alloc memory (else hipMemcpyAsync); max_blocks: its workgroups (0: one per 4 KB, up to
 // 1024).  RT_COPY_KERNEL / RT_COPY_BLOCKS override.
 static int copy_to_host(rt_ctx* c, void* host, const void* dev, size_t bytes, hipStream_t st, unsigned max_blocks = 0) {
     if (!bytes) return RT_OK;
-    void* dmap = pinned_device_ptr(host, bytes);
+    void* dmap = host_device_ptr(host, bytes);
     const bool kernel = c->copy_kernel != 0;
     if (dmap && kernel && ((uintptr_t)dmap | (uintptr_t)dev) % 16 == 0) {
         unsigned blocks = (unsigned)std::min<size_t>((bytes / 16 + kThreads - 1) / kThreads + 1, 1024);
