@@ -29,7 +29,15 @@ constexpr int kChunk = 4;              // spheres per branch-free filter batch
 #endif
 constexpr int kConeMin = RT_CONE_MIN;   // per-wave culling (primary cones, ray and shadow bundles) from this many (padded) spheres
 constexpr int kFastStride = kConeMin - kChunk;   // the array stride of every scene with np < kConeMin
-inline constexpr int sphere_stride(int np) { return np < kConeMin ? kFastStride : np; }
+// Scenes of kConeMin .. 64 (padded) spheres — the culling kernels' — have the fixed stride 64, which their kernel
+// instance sees as a constant (RT_CULL_FIX64; more spheres: stride np, the general instance).
+#ifndef RT_CULL_FIX64
+#define RT_CULL_FIX64 1
+#endif
+constexpr int kCullStride = 64;
+inline constexpr int sphere_stride(int np) {
+    return np < kConeMin ? kFastStride : (RT_CULL_FIX64 && np <= kCullStride ? kCullStride : np);
+}
 // The primary-ray cone mask is one ballot per wave (fast FP32 math): from 8 spheres it beats the per-sphere
 // FP32 filter batches it replaces (same-box A/B: c2 -0.8%, c3 -1.9%; from 4 spheres c1 +3.7%).
 #ifndef RT_PRIMARY_CONE_MIN

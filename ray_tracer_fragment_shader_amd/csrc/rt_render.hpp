@@ -250,7 +250,7 @@ __device__ __forceinline__ void store_pixel(const RenderParams& P, size_t k, d3 
 }
 
 template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false,
-          bool PACKED = false>
+          bool PACKED = false, bool FIX64 = false>
 __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene, RenderParams P,
                                             const int32_t* __restrict__ tile_rows,
                                             const uint64_t* __restrict__ cone_in) {
@@ -281,7 +281,8 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     if (LDS) __syncthreads();
     // the fast kernels (scenes with np < kConeMin) see the fixed array stride as a constant
     constexpr bool kFixed = !LDS && !TRANSP && !CULL && !TREE && WG == RT_WG_FAST && RT_WG_FAST != kThreads;
-    const SceneView V = view_of(S, gscene, P.np, kFixed ? kFastStride : P.ns, P.nl);
+    // (FIX64: the culling instance for scenes whose arrays have the stride kCullStride, see rt_layout.hpp)
+    const SceneView V = view_of(S, gscene, P.np, kFixed ? kFastStride : FIX64 ? kCullStride : P.ns, P.nl);
     const d3 eye = ld3(P.eye);
 
     const int wave = tid >> 6, lane = tid & 63;
@@ -433,12 +434,12 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
 
 // (out32 .. outrc are read by late_outputs() from the argument segment, not through the parameters)
 template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false,
-          bool PACKED = false>
+          bool PACKED = false, bool FIX64 = false>
 __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene, RenderParams P,
                                                              void* out32, void* out8, double* out64, uint32_t* outrc,
                                                              const int32_t* __restrict__ tile_rows,
                                                              const uint64_t* __restrict__ cone_in) {
-    render_body<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED>(gscene, P, tile_rows, cone_in);
+    render_body<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED, FIX64>(gscene, P, tile_rows, cone_in);
 }
 
 // The same kernel with its SGPRs capped at RT_FAST_SGPRS (amdgpu_num_sgpr: a constant, hence a kernel of its
@@ -588,9 +589,9 @@ RT_DECLARE_DEPTH(4) RT_DECLARE_DEPTH(5) RT_DECLARE_DEPTH(6) RT_DECLARE_DEPTH(7)
 #undef RT_DECLARE_DEPTH
 
 // Body of the per-depth instance files.
-template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG, bool TREE, bool PACKED = false>
+template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG, bool TREE, bool PACKED = false, bool FIX64 = false>
 hipError_t launch_render_one(const RenderLaunch& L) {
-    auto kern = rt_render_kernel<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED>;
+    auto kern = rt_render_kernel<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED, FIX64>;
     if (L.lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds);
         if (e != hipSuccess) return e;
@@ -623,8 +624,14 @@ hipError_t launch_render_impl(const RenderLaunch& L) {
                 if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return launch_render_sg<B, MW, false>(L);
                 return launch_render_one<B, 0, MW, false, false, RT_WG_FAST, false>(L);
             case kVarFastAnyW: return launch_render_one<B, 0, 1, false, false, RT_WG_FAST, false>(L);
-            case kVarCull: return launch_render_one<B, 0, cull_min_waves(B), false, true, RT_WG_FAST, false>(L);
-            case kVarCullAnyW: return launch_render_one<B, 0, 1, false, true, RT_WG_FAST, false>(L);
+            case kVarCull:
+                if (RT_CULL_FIX64 && L.P.ns == kCullStride)
+                    return launch_render_one<B, 0, cull_min_waves(B), false, true, RT_WG_FAST, false, false, true>(L);
+                return launch_render_one<B, 0, cull_min_waves(B), false, true, RT_WG_FAST, false>(L);
+            case kVarCullAnyW:
+                if (RT_CULL_FIX64 && L.P.ns == kCullStride)
+                    return launch_render_one<B, 0, 1, false, true, RT_WG_FAST, false, false, true>(L);
+                return launch_render_one<B, 0, 1, false, true, RT_WG_FAST, false>(L);
             case kVarTransp: return launch_render_one<B, 0, 1, true, false, 64, false>(L);
             case kVarTree: return launch_render_one<B, 0, 1, true, false, 64, true>(L);
             case kVarLds: return launch_render_one<B, 1, 1, false, false, kThreads, false>(L);
@@ -634,6 +641,9 @@ hipError_t launch_render_impl(const RenderLaunch& L) {
                 if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return launch_render_sg<B, MW, true>(L);
                 return launch_render_one<B, 0, (B <= 3 ? MW : 1), false, false, RT_WG_FAST, false, true>(L);
             case kVarCullPacked:
+                if (RT_CULL_FIX64 && L.P.ns == kCullStride)
+                    return launch_render_one<B, 0, (B <= 3 ? cull_min_waves(B) : 1), false, true, RT_WG_FAST, false, true,
+                                             true>(L);
                 return launch_render_one<B, 0, (B <= 3 ? cull_min_waves(B) : 1), false, true, RT_WG_FAST, false, true>(L);
             case kVarTranspPacked: return launch_render_one<B, 0, 1, true, false, 64, false, true>(L);
             case kVarTreePacked: return launch_render_one<B, 0, 1, true, false, 64, true, true>(L);
@@ -687,7 +697,7 @@ const void* render_kernel_ptr_impl(int variant) {
             case 0:
                 if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return (const void*)rt_render_kernel_sg<B, kFast, false, false>;
                 return (const void*)rt_render_kernel<B, 0, kFast, false, false, RT_WG_FAST, false>;
-            case 1: return (const void*)rt_render_kernel<B, 0, kCull, false, true, RT_WG_FAST, false>;
+            case 1: return (const void*)rt_render_kernel<B, 0, kCull, false, true, RT_WG_FAST, false, false, (bool)RT_CULL_FIX64>;
             case 2: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, false>;
             case 3: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, true>;
             default: return nullptr;
