@@ -51,7 +51,7 @@ int rt_trace_screen_dev(rt_ctx* c, const double cam[3], const ScreenPix* pix, co
                         void* stream);
 constexpr int kScreenMaxRays = 1 << 19;        // rays of one chunk
 constexpr int kScreenMaxPix = 4096;            // pixels of one chunk
-constexpr int kScreenMaxJit = kScreenMaxPix * 16 + 128;   // stream values of one chunk
+constexpr int kScreenMaxJit = kScreenMaxPix * 16 + kScreenMaxWindow;   // stream values of one chunk
 constexpr int kScreenMaxBlocks = (kScreenMaxRays + kScreenBlock - 1) / kScreenBlock;
 // Frees the rt_render_screen buffers kept for `ctx` (rt_ctx_destroy).
 void rt_screen_release(const rt_ctx* ctx);

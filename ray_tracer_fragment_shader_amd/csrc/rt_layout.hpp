@@ -175,7 +175,7 @@ struct ScreenPix {
     double sp[3];
     int32_t base, len, off, pad;
 };
-constexpr int kScreenMaxWindow = 128;          // len <= this
+constexpr int kScreenMaxWindow = 128;          // len <= this (the window half-width kWin <= 56)
 // (64-thread workgroups — one wave per CU for a small chunk — measured the same GPU wait per chunk as 256: the
 // latency is the trace's own instruction chain, not CU sharing)
 #ifndef RT_SCREEN_WG

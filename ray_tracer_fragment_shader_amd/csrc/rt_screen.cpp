@@ -308,10 +308,15 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // Chunks go to three buffer sets, each with its own stream: a dropped continuation finishes on its stream
     // beside the restarted chain instead of ahead of it, and its set is reused once it is done.  Resolution is
     // unchanged: every pixel reads its samples at its actual stream position, or breaks.
-    const int kMaxRays = kScreenMaxRays, kMaxPix = kScreenMaxPix, kWin = 28;
+    const int kMaxRays = kScreenMaxRays, kMaxPix = kScreenMaxPix;
     const int kMaxJit = kScreenMaxJit;
-    static_assert(16 + 2 * kWin <= kScreenMaxWindow, "window longer than a pixel table entry allows");
-    static_assert(kScreenMaxJit >= kScreenMaxPix * 16 + 2 * kWin + 16, "stream-value buffer too small");
+    constexpr int kWinMax = (kScreenMaxWindow - 16) / 2;
+    static_assert(kScreenMaxJit >= kScreenMaxPix * 16 + 2 * kWinMax + 16, "stream-value buffer too small");
+    // RT_SCREEN_WIN (A/B): the window half-width kWin (stream positions either side of a pixel's predicted range).
+    // 56 (the most a pixel table entry holds): fewer restarts for twice the traced colours; in-process A/B against
+    // r03's 28, demo -9.6%, c2 scene -14% (20: +33%; 36/44: -1 to -13%; 72/96/120 with larger tables: +2 to +34%).
+    int kWin = kWinMax;
+    if (const char* ev = getenv("RT_SCREEN_WIN")) kWin = std::min(std::max(atoi(ev), 16), kWinMax);
     // The buffers live in the context between calls (allocating ~40 MB of device and mapped host memory
     // per frame cost more than a quarter of a demo frame); a call running concurrently on the same context
     // allocates its own.
