@@ -2,7 +2,7 @@
 """Simulate rt_render_screen's chunk schedule (rt_screen.cpp) on the reference's own per-pixel sample counts
 (from the oracle's rayTraceScreen): round trips on the critical path, rays traced, dropped continuations.
 The actual stream position of a pixel is the prefix sum of the counts, so the schedule depends on nothing else.
-usage: screen_sim.py [scene W H] [--win 28] [--next 1] [--conf 0]"""
+usage: screen_sim.py [scene W H] [--win 56] [--next 1] [--conf 0]"""
 import argparse
 import os
 import sys
@@ -110,7 +110,7 @@ def simulate(cnt, W, win=28, next_mul=1, conf=0, max_pix=4096, max_rays=1 << 19)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("scene", nargs="*", default=["demo", "500", "500"])
-    ap.add_argument("--win", type=int, default=28)
+    ap.add_argument("--win", type=int, default=56)
     ap.add_argument("--next", type=int, default=1)
     ap.add_argument("--conf", type=int, default=0)
     a = ap.parse_args()
