@@ -161,6 +161,20 @@ struct Jitter {
     }
 };
 
+// length(d) < t (:1307) without the square root where the squares decide: s = |d|^2 is computed exactly as
+// length() computes it, and sqrt is correctly rounded and monotonic, so s < t^2 (1 - 2^-40) (t^2 itself within 2^-53)
+// puts sqrt(s) below t (1 - 2^-42), which rounds below t, and s > t^2 (1 + 2^-40) puts it above; only between the
+// two (and for t <= 0, inf or NaN operands, where both comparisons fail) is the square root taken.
+inline bool converged(V3 d, double t) {
+    const double s = d.x * d.x + d.y * d.y + d.z * d.z;
+    if (t > 0.0) {
+        const double tt = t * t;
+        if (s < tt * (1.0 - 0x1p-40)) return true;
+        if (s > tt * (1.0 + 0x1p-40)) return false;
+    }
+    return std::sqrt(s) < t;
+}
+
 inline unsigned char to_u8(double c) {
     double v = c < 0.0 ? 0.0 : (c > 1.0 ? 1.0 : c);
     return (unsigned char)(int)std::floor(v * 255.0 + 0.5);
@@ -369,6 +383,10 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     // but demo +4.7%, c2 scene -0.4% against waiting for the whole chunk (in-process A/B): the releases cost what the
     // overlap saves.  Off.
     bool progressive = false;
+    // RT_SCREEN_PREFETCH: resolve prefetches the colours of the pixel this many ahead at its predicted position (the
+    // GPU wrote them over PCIe: every pixel's first read would miss the host's caches).  0: off.
+    int prefetch = 8;
+    if (const char* ev = getenv("RT_SCREEN_PREFETCH")) prefetch = std::max(0, atoi(ev));
     if (const char* ev = getenv("RT_SCREEN_PROGRESSIVE")) progressive = atoi(ev) != 0;
     using clk = std::chrono::steady_clock;
     double t_build = 0, t_gen = 0, t_gpu = 0, t_res = 0;
@@ -551,6 +569,12 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
         for (; q < cur.m && !broke; ++q) {
             const ScreenPix& X = hp[q];
             if ((rc = wait_rays(X.off + X.len - 1))) return rc;
+            if (prefetch && q + prefetch < cur.m) {                   // the predicted samples of pixel q + prefetch
+                const ScreenPix& Y = hp[q + prefetch];
+                const double* y = hr + 3 * (size_t)(Y.off + std::min(Y.len - 1, kWin));
+                __builtin_prefetch(y);
+                __builtin_prefetch(y + 8);
+            }
             if (A < X.base) {                                        // the stream ran behind the window
                 broke = true;
                 break;
@@ -568,7 +592,7 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
                 const V3 oldWeightedColor = (k + 1.0) * avgColor;
                 avgColor = avgColor + color;                         // avgColor += color
                 const V3 weightedColor = k * avgColor;
-                if (length(weightedColor - oldWeightedColor) < small * k * (k + 1)) break;
+                if (converged(weightedColor - oldWeightedColor, small * k * (k + 1))) break;
             }
             if (need_more) {
                 avgColor = a0;
