@@ -306,6 +306,61 @@ def serial_kernel_ms(torch, L, abi, launch, stream, n=20):
     return e[0].elapsed_time(e[1]) / n
 
 
+HBM_PEAK_GBS = 8000.0
+
+
+def c4_scaling_keys(n, W, H, rays, c4_ms, c3_ms_inflight, c3_ms_serial):
+    """The c4 leg's scaling figures against the same job's one-GPU c3 frame (measured on rank 0 before the group
+    leg, same scene, view and RGBA8 output): speedup = one GPU's best c3 frame time (frames in flight) / the split
+    frame's time, efficiency = speedup / n; also against the one-stream serial c3 frame.  HBM-write fraction per GPU
+    = the RGBA8 image's bytes (W x H x 4) shared over n GPUs per split frame, against HBM_PEAK_GBS."""
+    out = {"c3_1gpu_ms_per_frame": round(c3_ms_inflight, 5), "c3_1gpu_ms_serial": round(c3_ms_serial, 5)}
+    if not c4_ms or c4_ms <= 0:
+        return out
+    sp = c3_ms_inflight / c4_ms
+    out.update({
+        "speedup_vs_c3_1gpu": round(sp, 3),
+        "efficiency": round(sp / n, 3),
+        "speedup_vs_c3_1gpu_serial": round(c3_ms_serial / c4_ms, 3),
+        "mray_s_per_gpu": round(rays / (c4_ms * 1e-3) / 1e6 / n, 3),
+        "hbm_write_frac_per_gpu": round((W * H * 4 / n) / (c4_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 5),
+    })
+    return out
+
+
+def c4_parallelism_text(n, c4):
+    """The top-level `parallelism` suffix that carries the row-split c4 curve at N > 1 (SCALE records)."""
+    if not c4 or "speedup_vs_c3_1gpu" not in c4:
+        return ""
+    return (f"; c4 (one 3840x2160 frame row-split over {n} GPUs, RGBA8 gathered to rank 0): {c4.get('value')} Mray/s, "
+            f"{c4['mray_s_per_gpu']} Mray/s per GPU, {c4['speedup_vs_c3_1gpu']}x one GPU's c3 frame "
+            f"(efficiency {c4['efficiency']}), HBM-write {c4['hbm_write_frac_per_gpu']} of peak per GPU")
+
+
+def c3_one_gpu(torch, L, abi, Tracer, cfg, dev, local, nfly, steps):
+    """One GPU's c3 frame as the c4 leg's denominator: RGBA8 only (the group leg's output), calibrated view, `nfly`
+    frames in flight on their own streams (the bench's timed pattern) and one stream serial.  -> (ms in flight, ms
+    serial)."""
+    W, H, B = cfg.width, cfg.height, cfg.depth
+    cam = cfg.camera()
+    ts = [Tracer(local) for _ in range(nfly)]
+    for t in ts:
+        t.set_scene(cfg.scene())
+    ss = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nfly - 1)]
+    outs = [torch.empty((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(nfly)]
+    la = [(ts[i]._ctx, ctypes.byref(cam), W, H, B, None, None, ctypes.c_void_p(outs[i].data_ptr()), None, None,
+           ctypes.c_void_p(ss[i].cuda_stream)) for i in range(nfly)]
+    for _ in range(2):                                       # first render + the calibration render of the view
+        for a in la:
+            abi.check(L.rt_render_dev(*a), "rt_render_dev")
+    torch.cuda.synchronize()
+    _, ms_fly = pipelined_frames(torch, L, abi, ts, ss, la, steps, 0.0)
+    ms_ser = serial_kernel_ms(torch, L, abi, la[0], ss[0], n=steps)
+    for t in ts:
+        t.close()
+    return ms_fly, ms_ser
+
+
 def packed_host_legs(t, sa, cam, W, H, B, k=30):
     """draw()'s host frame in the narrowest exact format (rt_render_packed, GRAY8 for the achromatic c2 scene:
     2.1 MB over PCIe instead of 8.3 MB), synchronous and pipelined (rt_render_packed_async + rt_ctx_wait: the copy of
@@ -527,15 +582,24 @@ def main() -> int:
         return int((rc & 0xFFFF).sum().item()) + int((rc >> 16).sum().item())
 
     # ---- one frame split over all ranks, RCCL gather to rank 0 (C ABI group) ----------------------------
-    def group_leg(cfg, steps, warmup):
+    def group_leg(cfg, steps, warmup, copy_ranks=0):
         """rt_render_multi over the job's ranks (one process per GPU: rt_group_create_rank; N = 1: a
-        one-rank RCCL group).  Returns (stats dict, seconds for `steps` frames, max over ranks)."""
+        one-rank RCCL group).  copy_ranks > 0 (gloo rehearsal on one GPU, rank 0 only): one process driving
+        `copy_ranks` contexts that share the device, COPY transport — the same group code, no xGMI.
+        Returns (stats dict, seconds for `steps` frames, max over ranks)."""
         W, H, B = cfg.width, cfg.height, cfg.depth
         cam = cfg.camera()
         t = Tracer(local)
         t.set_scene(cfg.scene())
         g = ctypes.c_void_p()
-        if world > 1:
+        extra = []
+        if copy_ranks:
+            extra = [Tracer(local) for _ in range(copy_ranks - 1)]
+            for e in extra:
+                e.set_scene(cfg.scene())
+            arr = (ctypes.c_void_p * copy_ranks)(t._ctx.value, *[e._ctx.value for e in extra])
+            abi.check(L.rt_group_create(arr, copy_ranks, abi.RT_TRANSPORT_COPY, ctypes.byref(g)), "rt_group_create")
+        elif world > 1:
             idt = torch.zeros(abi.RT_COMM_ID_BYTES, dtype=torch.uint8)
             if rank == 0:
                 abi.check(L.rt_comm_unique_id(ctypes.c_void_p(idt.data_ptr())), "rt_comm_unique_id")
@@ -547,8 +611,9 @@ def main() -> int:
         else:
             arr = (ctypes.c_void_p * 1)(t._ctx.value)
             abi.check(L.rt_group_create(arr, 1, abi.RT_TRANSPORT_RCCL, ctypes.byref(g)), "rt_group_create")
+        gw = copy_ranks or world                           # ranks of the group
         band, slab = ctypes.c_int(), ctypes.c_int()
-        abi.check(L.rt_band_plan(H, world, args.band_height, ctypes.byref(band), ctypes.byref(slab)), "rt_band_plan")
+        abi.check(L.rt_band_plan(H, gw, args.band_height, ctypes.byref(band), ctypes.byref(slab)), "rt_band_plan")
         img8 = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
         argv = (g, ctypes.byref(cam), W, H, B, args.band_height, abi.RT_OUT_RGBA8,
                 None, ctypes.c_void_p(img8.data_ptr()) if img8 is not None else None, ctypes.c_void_p(stream.cuda_stream))
@@ -561,15 +626,17 @@ def main() -> int:
         for _ in range(max(warmup, 20)):                  # includes the tile-order calibration of every rank
             abi.check(fn(*argv), "rt_render_multi")
         sync()
-        barrier()
+        if not copy_ranks:
+            barrier()
         t0 = time.perf_counter()
         for _ in range(steps):
             rc = fn(*argv)
             if rc:
                 abi.check(rc, "rt_render_multi")
         sync()
-        barrier()
-        elapsed = max_over_ranks(time.perf_counter() - t0)
+        if not copy_ranks:
+            barrier()
+        elapsed = time.perf_counter() - t0 if copy_ranks else max_over_ranks(time.perf_counter() - t0)
         # per-phase times (HIP events on the group's render / comm streams), in a separate untimed pass so the
         # events do not perturb the timed one
         abi.check(L.rt_group_timing(g, 1), "rt_group_timing")
@@ -578,10 +645,12 @@ def main() -> int:
         st = abi.rt_group_stats()
         abi.check(L.rt_group_get_stats(g, ctypes.byref(st)), "rt_group_get_stats")
         torch.cuda.synchronize()
-        barrier()
+        if not copy_ranks:
+            barrier()
         phases = {"render_ms": st.render_ms, "gather_ms": st.gather_ms, "assemble_ms": st.assemble_ms,
                   "frame_ms": st.frame_ms}
-        phases_max = {k: round(max_over_ranks(v), 5) for k, v in phases.items()}
+        phases_max = ({k: round(v, 5) for k, v in phases.items()} if copy_ranks else
+                      {k: round(max_over_ranks(v), 5) for k, v in phases.items()})
         names = {abi.RT_PIXEL_GRAY8: "GRAY8", abi.RT_PIXEL_RGB8: "RGB8", abi.RT_PIXEL_RGBA8: "RGBA8", -1: None}
         parity = None
         if rank == 0:                                      # gathered frame == one-launch frame, every byte
@@ -591,7 +660,11 @@ def main() -> int:
         rays = frame_rays(t, cam, W, H, B) if rank == 0 else 0
         L.rt_group_destroy(g)
         t.close()
-        info = {"ranks": world, "rccl_world": world, "transport": "RCCL", "band_height": band.value,
+        for e in extra:
+            e.close()
+        info = {"ranks": gw, "rccl_world": 0 if copy_ranks else world,
+                "transport": "COPY (rehearsal: contexts share one GPU)" if copy_ranks else "RCCL",
+                "band_height": band.value,
                 "slab_rows": slab.value, "rays_per_frame": rays, "parity": parity,
                 "wire_format": names.get(st.wire_byte, st.wire_byte), "payload_bytes_to_rank0": st.payload_bytes,
                 "phases_ms_rank0": {k: round(v, 5) for k, v in phases.items()} if rank == 0 else None,
@@ -813,6 +886,7 @@ def main() -> int:
                                 f"row bands (h={plan.band_height}) x {world} ranks + RCCL gather to rank 0 "
                                 f"(rt_render_multi)" if strong else
                                 f"{world} ranks x whole frames (independent frames, no collective)"
+                                + c4_parallelism_text(world, res_extra.get("c4"))
                                 if world > 1 else "single GPU"),
             },
             "roofline": roof,
@@ -822,7 +896,7 @@ def main() -> int:
         res.update(res_extra)
         return res
 
-    if extra_ok and not args.no_c4 and not strong and not rehearsal:
+    if extra_ok and not args.no_c4 and not strong:
         # Guarded: the timed metric above is already final.  A failure of this leg is reported in its
         # entry; a leg that does not finish within --c4-timeout seconds (e.g. a peer that never joins the
         # RCCL gather) ends the job with the line as it stands rather than leaving it without one, and with
@@ -841,17 +915,33 @@ def main() -> int:
         try:
             c3 = scenes.CONFIGS["c3"]
             steps4 = max(10, min(args.steps, 40))
-            info, el4 = group_leg(c3, steps4, 3)
+            # the denominator of the split frame's speed-up: the same job's one-GPU c3 frame (same scene, view and
+            # RGBA8 output), measured on rank 0 before the group leg at every N
+            base = (c3_one_gpu(torch, L, abi, Tracer, c3, dev, local, max(1, args.frames_in_flight), steps4)
+                    if rank == 0 else None)
+            barrier()
+            if rehearsal:                                   # gloo on one GPU: rank 0 drives `world` COPY ranks
+                info, el4 = group_leg(c3, steps4, 3, copy_ranks=world) if rank == 0 else ({}, 0.0)
+                barrier()
+            else:
+                info, el4 = group_leg(c3, steps4, 3)
             info.update({"workload": "c4: c3's 3840x2160 frame (8 spheres + board, 2 lights, 2 bounces) split "
                                      f"over {world} rank(s) in round-robin row bands, RGBA8 gathered to rank 0 over "
                                      "RCCL (ncclSend/ncclRecv in rt_render_multi) and unshuffled there"
                                      if world > 1 else
                                      "c4 machinery at one rank: c3's 3840x2160 frame through rt_render_multi of a "
                                      "one-rank RCCL group (identity band plan: rendered straight into the image)",
-                         "frames": steps4, "ms_per_frame": round(el4 / steps4 * 1e3, 4),
+                         "frames": steps4, "ms_per_frame": round(el4 / steps4 * 1e3, 4) if el4 else None,
                          "value": (round(info["rays_per_frame"] * steps4 / el4 / 1e6, 3)
                                    if rank == 0 and "error" not in info else None),
                          "unit": "Mray/s", "scaling": "strong"})
+            if rank == 0 and base and "error" not in info:
+                info.update(c4_scaling_keys(info["ranks"], c3.width, c3.height, info["rays_per_frame"],
+                                            el4 / steps4 * 1e3, *base))
+                info["scaling_note"] = ("speedup_vs_c3_1gpu = c3_1gpu_ms_per_frame (one GPU, RGBA8 only, "
+                                        f"{max(1, args.frames_in_flight)} frames in flight, measured on rank 0 of this "
+                                        "job before the group leg) / ms_per_frame; efficiency = speedup / ranks; "
+                                        "hbm_write_frac_per_gpu = (W x H x 4 B / ranks) / ms_per_frame / 8 TB/s")
             res_extra["c4"] = info
         except Exception as exc:                            # reported, the timed metric stands
             res_extra["c4"] = {"error": f"{type(exc).__name__}: {exc}"}

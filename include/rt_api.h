@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 #define RT_OK            0
 #define RT_EINVAL       -1   /* bad argument (null pointer, size, unsupported material, ...) */
@@ -319,6 +319,30 @@ typedef struct rt_group rt_group;
 /* Bands for n_ranks: band_height 0 = auto (largest height <= 16 that gives every rank the same rows, e.g.
  * 15 for 1080 rows over 8 ranks; else 8).  *slab_rows_out (nullable) = the most rows any rank renders. */
 int rt_band_plan(int height, int n_ranks, int band_height, int* band_out, int* slab_rows_out);
+/* What one rank of a row-banded frame moves (host only, no device: the plan rt_render_multi follows).
+ * kind 0 = the RGBA32F image, 1 = the RGBA8 image (RT_OUT_RGBA32F / RT_OUT_RGBA8). */
+typedef struct rt_group_plan {
+    int32_t n_ranks, rank;
+    int32_t band_height;         /* rt_band_plan */
+    int32_t slab_rows;           /* the most rows any rank renders */
+    int32_t rank_rows;           /* rows this rank renders (rt_local_rows) */
+    int32_t wire[2];             /* RT_PIXEL_* the kind travels in (GRAY for achromatic scenes), -1: not requested */
+    int32_t elem_bytes[2];       /* bytes per pixel of wire[k] */
+    uint64_t slab_bytes[2];      /* this rank's slab per kind: slab_rows x width x elem_bytes */
+    uint64_t send_bytes[2];      /* bytes this rank sends rank 0 per frame (0 on rank 0: its slab is unpacked in place) */
+    uint64_t gather_bytes[2];    /* rank 0: its gather buffer per kind (n_ranks slab-sized slots) */
+    uint64_t payload_bytes;      /* rank 0: bytes received from the other ranks per frame, all kinds */
+} rt_group_plan;
+/* The plan of `rank` for a width x height frame (band_height 0 = auto, `outputs` as rt_render_multi, achromatic =
+ * rt_scene_achromatic of the group's scene). */
+int rt_group_plan_frame(int width, int height, int n_ranks, int rank, int band_height, int outputs, int achromatic,
+                        rt_group_plan* out);
+/* Rank 0's receive from `peer` (1 .. n_ranks - 1) for image `kind`: byte offset into rank 0's gather buffer and
+ * byte count (equal to that peer's send_bytes[kind]). */
+int rt_group_plan_recv(const rt_group_plan* plan, int width, int height, int peer, int kind, uint64_t* offset,
+                       uint64_t* bytes);
+/* FNV-1a 64 of the scene's flattened device record: what the ranks of a one-process-per-GPU group compare. */
+int rt_scene_fingerprint(const rt_scene* scene, uint64_t* out);
 /* One process driving n GPUs: ctxs[q] is rank q (ctxs[0] receives the image); distinct contexts, each on
  * its device (ncclCommInitAll over the contexts' devices for RT_TRANSPORT_RCCL). */
 int rt_group_create(rt_ctx* const* ctxs, int n, int transport, rt_group** out);
@@ -339,8 +363,10 @@ int rt_group_info(const rt_group* group, int* n_ranks, int* n_local, int* first_
  * each rank from its own context's scene — they are the same scene) GRAY8 for RGBA8 and GRAY32F for RGBA32F,
  * otherwise RGB8 and RGBA32F; rank 0 expands them into its images (rt_unpack_dev), byte for byte the images a
  * single rt_render_dev writes.  Every rank changes its scene (rt_set_scene) between the same frames; in a
- * one-process-per-GPU group the first frame after a rank's scene changed all-reduces a fingerprint of the
- * scene over the group (blocking, once per scene) and fails with RT_EINVAL on every rank when they differ. */
+ * one-process-per-GPU group the first frame after a rank's scene differs from the one the group last agreed on
+ * all-reduces a fingerprint of the scene over the group (blocking, once per scene) and fails with RT_EINVAL on
+ * every rank when they differ.  A scene change on some ranks only (the others still holding the agreed scene) is a
+ * contract violation: those ranks enter the all-reduce while the others post their sends, and the group HANGS. */
 int rt_render_multi(rt_group* group, const rt_camera* cam, int width, int height, int depth, int band_height,
                     int outputs, float* rgba32f, uint8_t* rgba8, void* stream);
 /* Wait for the group's own render and gather streams (e.g. before timing on a rank > 0). */

@@ -23,6 +23,17 @@ extern "C" {
  * Asynchronous on `stream`.  RT_EINVAL for an unknown op or null buffers. */
 int rt_probe_math_dev(int op, const double* in, int n, double* out, void* stream);
 
+/* The scene agreement of a one-process-per-GPU group (rt_render_multi), without its collective, so the CPU tests
+ * drive it from several processes.  rt_group_agree_due: 1 when a rank whose scene has `fingerprint` must vote
+ * before its next frame (it differs from the last agreed one, or nothing was agreed yet).  rt_group_agree_vote:
+ * this rank's vote {h, ~h, a, ~a}.  rt_group_agree_combine: acc = element-wise unsigned max(acc, other) — what the
+ * group's ncclAllReduce(ncclMax) computes.  rt_group_agree_verdict: RT_OK when the combined votes of every rank
+ * name one scene (fingerprint and achromatic flag), else RT_EINVAL. */
+int rt_group_agree_due(uint64_t fingerprint, int agreed, uint64_t agreed_fingerprint);
+void rt_group_agree_vote(uint64_t fingerprint, int achromatic, uint64_t vote[4]);
+void rt_group_agree_combine(uint64_t acc[4], const uint64_t other[4]);
+int rt_group_agree_verdict(const uint64_t reduced[4]);
+
 /* Tile-row dispatch order of later rt_render_dev calls of this context: mode 0 (default) adaptive — the
  * first render of a new (scene, camera, size, row plan, depth) times its 8-row tile rows and later
  * renders dispatch them longest first; mode 1 bottom-to-top.  Images are identical either way (every

@@ -26,7 +26,7 @@ RT_MAX_DEPTH = 7
 RT_RAND_GLIBC, RT_RAND_MSVC = 0, 1
 RT_MESH_TETRAHEDRON = 1
 RT_MESH_CUBE = 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 RT_TRANSPORT_AUTO, RT_TRANSPORT_RCCL, RT_TRANSPORT_COPY = -1, 0, 1
 RT_OUT_RGBA32F, RT_OUT_RGBA8 = 1, 2
 RT_PIXEL_RGBA32F, RT_PIXEL_GRAY32F, RT_PIXEL_RGBA8, RT_PIXEL_RGB8, RT_PIXEL_GRAY8 = 0, 1, 2, 3, 4
@@ -103,6 +103,13 @@ class rt_group_stats(Structure):
                 ("assemble_ms", c_double), ("frame_ms", c_double)]
 
 
+class rt_group_plan(Structure):
+    _fields_ = [("n_ranks", c_int32), ("rank", c_int32), ("band_height", c_int32), ("slab_rows", c_int32),
+                ("rank_rows", c_int32), ("wire", c_int32 * 2), ("elem_bytes", c_int32 * 2),
+                ("slab_bytes", c_uint64 * 2), ("send_bytes", c_uint64 * 2), ("gather_bytes", c_uint64 * 2),
+                ("payload_bytes", c_uint64)]
+
+
 class RtError(RuntimeError):
     def __init__(self, code: int, where: str, msg: str):
         super().__init__(f"{where}: rt error {code}: {msg}")
@@ -159,7 +166,14 @@ SIGNATURES = {
     "rt_host_alloc": (c_int, [ctypes.c_size_t, _P(c_void_p)]),
     "rt_host_free": (c_int, [c_void_p]),
     "rt_unpack_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "rt_group_plan_frame": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, _P(rt_group_plan)]),
+    "rt_group_plan_recv": (c_int, [_P(rt_group_plan), c_int, c_int, c_int, c_int, _P(c_uint64), _P(c_uint64)]),
+    "rt_scene_fingerprint": (c_int, [_P(rt_scene), _P(c_uint64)]),
     # include/rt_diag.h
+    "rt_group_agree_due": (c_int, [c_uint64, c_int, c_uint64]),
+    "rt_group_agree_vote": (None, [c_uint64, c_int, _P(c_uint64)]),
+    "rt_group_agree_combine": (None, [_P(c_uint64), _P(c_uint64)]),
+    "rt_group_agree_verdict": (c_int, [_P(c_uint64)]),
     "rt_probe_math_dev": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "rt_diag_tile_order": (c_int, [c_void_p, c_int]),
     "rt_diag_kernel_resources": (c_int, [c_int, c_int, _P(c_int), _P(c_int)]),

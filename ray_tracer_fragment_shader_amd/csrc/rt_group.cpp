@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "../../include/rt_api.h"
+#include "../../include/rt_diag.h"
 #include "rt_internal.hpp"
 
 namespace {
@@ -65,7 +66,7 @@ struct Rank {
     size_t slab_cap[2][kKinds] = {{0, 0}, {0, 0}};
     ncclComm_t comm = nullptr;
     uint64_t* d_agree = nullptr;               // rt_group_create_rank: the scene agreement's all-reduce buffer
-    uint64_t agreed_gen = 0;                   // the context's scene generation the group last agreed on
+    uint64_t agreed_fp = 0;                    // the scene fingerprint the group last agreed on
     bool agreed = false;
     PhaseEvents ph[kRing];
 };
@@ -370,28 +371,30 @@ extern "C" int rt_group_get_stats(rt_group* g, rt_group_stats* st) {
 
 // One process per GPU (rt_group_create_rank): each rank picks its wire formats from its own context's scene, so
 // the ranks must hold the same scene or the byte counts of ncclSend / ncclRecv disagree (a hang or a torn frame).
-// Whenever this rank's scene generation changed since the last agreement — every rank changes its scene between
-// the same frames (include/rt_api.h, rt_render_multi) — the group all-reduces (max) {h, ~h, a, ~a} of the scene
-// fingerprint h and the achromatic flag a: every rank then sees min = max for both, or fails with RT_EINVAL.
+// Whenever this rank's scene differs from the one the group last agreed on — every rank changes its scene between
+// the same frames (include/rt_api.h, rt_render_multi) — the group all-reduces (max) the ranks' votes
+// {h, ~h, a, ~a} of the scene fingerprint h and the achromatic flag a: every rank then sees min = max for both, or
+// fails with RT_EINVAL.  The decisions are rt_group_plan.cpp's (rt_group_agree_*), driven without a GPU by the
+// CPU tests; this function only adds the collective.
 int agree_on_scene(rt_group* g, Rank& r, int achro) {
+    (void)g;
     uint64_t gen = 0, h = 0;
     rt_ctx_scene_id(r.ctx, &gen, &h);
-    if (r.agreed && gen == r.agreed_gen) return RT_OK;
+    if (!rt_group_agree_due(h, r.agreed ? 1 : 0, r.agreed_fp)) return RT_OK;
     G_HIP(hipSetDevice(r.device));
     if (!r.d_agree && hipMalloc(&r.d_agree, 4 * sizeof(uint64_t)) != hipSuccess)
         return rt_fail(RT_ENOMEM, "rt_render_multi: hipMalloc of the scene agreement buffer failed");
-    const uint64_t a = (uint64_t)achro;
-    uint64_t v[4] = {h, ~h, a, ~a};
+    uint64_t v[4];
+    rt_group_agree_vote(h, achro, v);
     // on the comm stream, behind the previous frames' exchanges (collectives run in the same order on every rank)
     G_HIP(hipMemcpyAsync(r.d_agree, v, sizeof(v), hipMemcpyHostToDevice, r.cs));
     G_NCCL(ncclAllReduce(r.d_agree, r.d_agree, 4, ncclUint64, ncclMax, r.comm, r.cs));
     G_HIP(hipMemcpyAsync(v, r.d_agree, sizeof(v), hipMemcpyDeviceToHost, r.cs));
     G_HIP(hipStreamSynchronize(r.cs));
-    if (v[0] != ~v[1] || v[2] != ~v[3])
-        return rt_fail(RT_EINVAL, "rt_render_multi: the group's ranks hold different scenes (wire formats would "
-                                  "disagree); call rt_set_scene with the same scene on every rank");
+    int rc = rt_group_agree_verdict(v);
+    if (rc) return rc;
     r.agreed = true;
-    r.agreed_gen = gen;
+    r.agreed_fp = h;
     return RT_OK;
 }
 
@@ -407,9 +410,7 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     void* outs[kKinds] = {rgba32f, rgba8};
     if (g->owns_root && ((kind_on[0] && !rgba32f) || (kind_on[1] && !rgba8)))
         return rt_fail(RT_EINVAL, "rt_render_multi: rank 0 needs a device image for every requested output");
-    int hb = 0, slab_rows = 0;
-    int rc = rt_band_plan(H, g->n_ranks, band_height, &hb, &slab_rows);
-    if (rc) return rc;
+    int rc = RT_OK;
     const int b = (int)(g->frame & 1);
     const int slot = (int)(g->frame % kRing);
     const hipStream_t st = (hipStream_t)stream;
@@ -421,14 +422,18 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     // ... and across the processes of a one-process-per-GPU group
     if (g->n_ranks > 1 && (int)g->ranks.size() < g->n_ranks && (rc = agree_on_scene(g, g->ranks[0], achro)))
         return rc;
+    // What every rank sends and where rank 0's receives land: the host-only plan (rt_group_plan.cpp), one per local
+    // rank, plus rank 0's (its receive table and payload) — the same plan the CPU tests check across processes.
+    std::vector<rt_group_plan> plan(g->ranks.size());
+    for (size_t q = 0; q < g->ranks.size(); ++q)
+        if ((rc = rt_group_plan_frame(W, H, g->n_ranks, g->ranks[q].rank, band_height, outputs, achro, &plan[q])))
+            return rc;
+    rt_group_plan root_plan;
+    if ((rc = rt_group_plan_frame(W, H, g->n_ranks, 0, band_height, outputs, achro, &root_plan))) return rc;
+    const int hb = root_plan.band_height, slab_rows = root_plan.slab_rows;
+    // (the render call takes a format for an image it does not write too)
     const int wire[kKinds] = {achro ? RT_PIXEL_GRAY32F : RT_PIXEL_RGBA32F, achro ? RT_PIXEL_GRAY8 : RT_PIXEL_RGB8};
-    size_t elem[kKinds];
-    for (int k = 0; k < kKinds; ++k) {
-        int pb = 0;
-        rt_pixel_bytes(wire[k], &pb);
-        elem[k] = (size_t)pb;
-        g->last_wire[k] = kind_on[k] ? wire[k] : -1;
-    }
+    for (int k = 0; k < kKinds; ++k) g->last_wire[k] = root_plan.wire[k];
 
     // ---- one rank: the band plan is the identity, so the frame is rendered straight into the caller's image
     // on the caller's stream (no slab, no unshuffle, no cross-stream hand-off: each one costs ~30 us) ----
@@ -460,12 +465,12 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     // receive on the root, a send on a rank, the root's unshuffle): wait for the group and the caller's stream
     // first, whatever changed (width, band plan, outputs, wire format). ----
     bool must_grow = false;
-    for (auto& r : g->ranks)
+    for (size_t q = 0; q < g->ranks.size(); ++q)
         for (int k = 0; k < kKinds; ++k)
-            must_grow |= kind_on[k] && (size_t)slab_rows * W * elem[k] > r.slab_cap[b][k];
+            must_grow |= kind_on[k] && plan[q].slab_bytes[k] > g->ranks[q].slab_cap[b][k];
     if (g->owns_root)
         for (int k = 0; k < kKinds; ++k)
-            must_grow |= kind_on[k] && (size_t)g->n_ranks * slab_rows * W * elem[k] > g->gathered_cap[b][k];
+            must_grow |= kind_on[k] && root_plan.gather_bytes[k] > g->gathered_cap[b][k];
     if (must_grow && g->frame > 0) {
         rc = rt_group_synchronize(g);
         if (rc) return rc;
@@ -476,17 +481,16 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     }
     g->last_band = hb;
     g->last_slab_rows = slab_rows;
-    for (auto& r : g->ranks) {
+    for (size_t q = 0; q < g->ranks.size(); ++q) {
+        Rank& r = g->ranks[q];
         G_HIP(hipSetDevice(r.device));
         for (int k = 0; k < kKinds; ++k)
-            if (kind_on[k] && (rc = grow(&r.slab[b][k], &r.slab_cap[b][k], (size_t)slab_rows * W * elem[k])))
-                return rc;
+            if (kind_on[k] && (rc = grow(&r.slab[b][k], &r.slab_cap[b][k], plan[q].slab_bytes[k]))) return rc;
     }
     if (g->owns_root) {
         G_HIP(hipSetDevice(g->ranks[0].device));
         for (int k = 0; k < kKinds; ++k)
-            if (kind_on[k] && (rc = grow(&g->gathered[b][k], &g->gathered_cap[b][k],
-                                         (size_t)g->n_ranks * slab_rows * W * elem[k])))
+            if (kind_on[k] && (rc = grow(&g->gathered[b][k], &g->gathered_cap[b][k], root_plan.gather_bytes[k])))
                 return rc;
     }
     std::vector<PhaseEvents*> pe(g->ranks.size(), nullptr);
@@ -512,17 +516,11 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     }
 
     // ---- gather to rank 0 ------------------------------------------------------------------------------------
-    auto rows_of = [&](int q) {
-        rt_rows rr = {hb, g->n_ranks, q, 1};
-        int nl = 0;
-        rt_local_rows(H, &rr, &nl);
-        return nl;
+    // rank 0's receive from peer q for image k: offset into gathered[b][k] and bytes (= q's send_bytes[k])
+    auto recv_of = [&](int q, int k, uint64_t* off, uint64_t* bytes) {
+        return rt_group_plan_recv(&root_plan, W, H, q, k, off, bytes);
     };
-    uint64_t payload = 0;
-    for (int q = 1; q < g->n_ranks; ++q)
-        for (int k = 0; k < kKinds; ++k)
-            if (kind_on[k]) payload += (uint64_t)rows_of(q) * W * elem[k];
-    g->last_payload = payload;
+    g->last_payload = root_plan.payload_bytes;
     if (g->owns_root) {
         Rank& root = g->ranks[0];
         G_HIP(hipSetDevice(root.device));
@@ -538,20 +536,24 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
             if (pe[q]) G_HIP(hipEventRecord(pe[q]->g0, r.cs));
         }
         G_NCCL(ncclGroupStart());
-        for (auto& r : g->ranks) {
+        for (size_t lq = 0; lq < g->ranks.size(); ++lq) {
+            Rank& r = g->ranks[lq];
             for (int k = 0; k < kKinds; ++k) {
                 if (!kind_on[k]) continue;
-                const size_t bytes = (size_t)rows_of(r.rank) * W * elem[k];
                 ncclResult_t e = ncclSuccess;
-                if (r.rank != 0) e = ncclSend(r.slab[b][k], bytes, ncclUint8, 0, r.comm, r.cs);
+                if (r.rank != 0) e = ncclSend(r.slab[b][k], plan[lq].send_bytes[k], ncclUint8, 0, r.comm, r.cs);
                 if (e != ncclSuccess) {
                     (void)ncclGroupEnd();
                     return rt_fail(RT_EHIP, std::string("ncclSend: ") + ncclGetErrorString(e));
                 }
                 if (r.rank != 0) continue;
                 for (int q = 1; q < g->n_ranks; ++q) {        // the root's own slab is unshuffled in place
-                    char* dst = (char*)g->gathered[b][k] + (size_t)q * slab_rows * W * elem[k];
-                    e = ncclRecv(dst, (size_t)rows_of(q) * W * elem[k], ncclUint8, q, r.comm, r.cs);
+                    uint64_t off = 0, bytes = 0;
+                    if ((rc = recv_of(q, k, &off, &bytes))) {
+                        (void)ncclGroupEnd();
+                        return rc;
+                    }
+                    e = ncclRecv((char*)g->gathered[b][k] + off, bytes, ncclUint8, q, r.comm, r.cs);
                     if (e != ncclSuccess) {
                         (void)ncclGroupEnd();
                         return rt_fail(RT_EHIP, std::string("ncclRecv: ") + ncclGetErrorString(e));
@@ -581,9 +583,10 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
             if (r.rank != 0) G_HIP(hipStreamWaitEvent(root.cs, r.rendered[b], 0));
             for (int k = 0; k < kKinds; ++k) {
                 if (!kind_on[k] || r.rank == 0) continue;      // the root's own slab is unshuffled in place
-                char* dst = (char*)g->gathered[b][k] + (size_t)r.rank * slab_rows * W * elem[k];
-                G_HIP(hipMemcpyPeerAsync(dst, root.device, r.slab[b][k], r.device,
-                                         (size_t)rows_of(r.rank) * W * elem[k], root.cs));
+                uint64_t off = 0, bytes = 0;
+                if ((rc = recv_of(r.rank, k, &off, &bytes))) return rc;
+                G_HIP(hipMemcpyPeerAsync((char*)g->gathered[b][k] + off, root.device, r.slab[b][k], r.device, bytes,
+                                         root.cs));
             }
             G_HIP(hipEventRecord(r.sent[b], root.cs));
             r.sent_rec[b] = true;

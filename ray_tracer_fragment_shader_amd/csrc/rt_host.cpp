@@ -233,6 +233,18 @@ extern "C" int rt_global_row(int height, const rt_rows* r, int local_row, int* o
 }
 
 // Row bands of the multi-GPU group (rt_group.cpp).
+extern "C" int rt_pixel_bytes(int format, int* bytes) {
+    if (!bytes) return rt_fail(RT_EINVAL, "rt_pixel_bytes: null pointer");
+    switch (format) {
+        case RT_PIXEL_RGBA32F: *bytes = 16; return RT_OK;
+        case RT_PIXEL_GRAY32F: *bytes = 4; return RT_OK;
+        case RT_PIXEL_RGBA8: *bytes = 4; return RT_OK;
+        case RT_PIXEL_RGB8: *bytes = 3; return RT_OK;
+        case RT_PIXEL_GRAY8: *bytes = 1; return RT_OK;
+        default: *bytes = 0; return rt_fail(RT_EINVAL, "rt_pixel_bytes: unknown pixel format");
+    }
+}
+
 extern "C" int rt_band_plan(int height, int n_ranks, int band_height, int* band_out, int* slab_rows_out) {
     if (height <= 0 || n_ranks <= 0 || band_height < 0 || !band_out)
         return rt_fail(RT_EINVAL, "rt_band_plan: bad arguments");

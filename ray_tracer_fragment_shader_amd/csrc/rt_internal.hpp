@@ -12,6 +12,9 @@
 // Record `msg` as this thread's rt_last_error() and return `code`.
 int rt_fail(int code, const std::string& msg);
 
+// FNV-1a 64 of a flattened scene record (rt_scene_fingerprint; the context's scene_hash).
+uint64_t rt_blob_fingerprint(const std::vector<unsigned char>& blob);
+
 // Validate an rt_scene and flatten it into the device record (rt::DevScene followed by the spheres),
 // precomputing every derived quantity with the reference's operation order.
 int rt_build_dev_scene(const rt_scene* scene, std::vector<unsigned char>* blob);
@@ -28,7 +31,7 @@ int rt_ctx_achromatic(const rt_ctx* ctx);
 
 // The context's scene generation (changes with every rt_set_scene that uploads a different scene) and a
 // fingerprint of the uploaded record (FNV-1a of the flattened scene): rt_group.cpp agrees on the scene — hence
-// on the wire formats — across the processes of a group whenever a rank's generation changes.
+// on the wire formats — across the processes of a group whenever a rank's fingerprint differs from the agreed one.
 void rt_ctx_scene_id(const rt_ctx* ctx, uint64_t* gen, uint64_t* fingerprint);
 
 // rt_unshuffle_dev with rank 0's rows read from `rank0_slab` instead of the gathered buffer (the group's root

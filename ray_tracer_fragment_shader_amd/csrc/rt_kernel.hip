@@ -601,9 +601,7 @@ extern "C" int rt_set_scene(rt_ctx* c, const rt_scene* scene) {
     c->eye_valid = false;
     c->scene_set = true;
     c->blob.swap(blob);
-    uint64_t fp = 0xcbf29ce484222325ull;
-    for (unsigned char byte : c->blob) fp = (fp ^ byte) * 0x100000001b3ull;
-    c->scene_hash = fp;
+    c->scene_hash = rt_blob_fingerprint(c->blob);
     ++c->scene_gen;
     return RT_OK;
 }
@@ -668,18 +666,6 @@ static int render_params(const rt_ctx* c, const rt_camera* cam, int W, int H, in
 
 static bool float_format(int f) { return f == RT_PIXEL_RGBA32F || f == RT_PIXEL_GRAY32F; }
 static bool byte_format(int f) { return f == RT_PIXEL_RGBA8 || f == RT_PIXEL_RGB8 || f == RT_PIXEL_GRAY8; }
-
-extern "C" int rt_pixel_bytes(int format, int* bytes) {
-    if (!bytes) return rt_fail(RT_EINVAL, "rt_pixel_bytes: null pointer");
-    switch (format) {
-        case RT_PIXEL_RGBA32F: *bytes = 16; return RT_OK;
-        case RT_PIXEL_GRAY32F: *bytes = 4; return RT_OK;
-        case RT_PIXEL_RGBA8: *bytes = 4; return RT_OK;
-        case RT_PIXEL_RGB8: *bytes = 3; return RT_OK;
-        case RT_PIXEL_GRAY8: *bytes = 1; return RT_OK;
-        default: *bytes = 0; return rt_fail(RT_EINVAL, "rt_pixel_bytes: unknown pixel format");
-    }
-}
 
 // The device render behind rt_render_dev / rt_render_dev_packed: the float image (fmt_f) and the byte image
 // (fmt_8) in their formats, the FP64 colour and the ray counters, each nullable.

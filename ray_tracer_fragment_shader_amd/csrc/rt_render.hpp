@@ -366,6 +366,10 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
         col = trace_tree<B>(V, eye, sp, &seg, &sh);
     else
         col = trace<B, true, TRANSP, CULL, WG>(V, eye, sp, cone, &seg, &sh, slot, mslot);
+#if RT_WAVE_TRACE >= 2
+    asm volatile("" ::"v"(col.x), "v"(col.y), "v"(col.z));
+    const uint64_t t_trace = __builtin_amdgcn_s_memrealtime();   // trace() done, the stores next
+#endif
 
     if (WG != kThreads || !P.wg_staging) {
         // Direct stores: each wave writes its 8 x 8 block as 8 row segments (128 B of RGBA32F each) and
@@ -394,8 +398,9 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
             P.wtrace[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
             P.wtrace[4 * w + 3] = t_mid;
 #if RT_WAVE_TRACE >= 2
-            P.wtrace[4 * (size_t)P.tile_rows_n * gridDim.x + 2 * w] = t_ty;
-            P.wtrace[4 * (size_t)P.tile_rows_n * gridDim.x + 2 * w + 1] = t_cone;
+            P.wtrace[4 * (size_t)P.tile_rows_n * gridDim.x + 3 * w] = t_ty;
+            P.wtrace[4 * (size_t)P.tile_rows_n * gridDim.x + 3 * w + 1] = t_cone;
+            P.wtrace[4 * (size_t)P.tile_rows_n * gridDim.x + 3 * w + 2] = t_trace;
 #endif
             P.wtrace[4 * w + 2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
                                   ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);

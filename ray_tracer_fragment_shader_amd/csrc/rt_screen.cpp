@@ -165,9 +165,11 @@ struct Jitter {
 // length() computes it, and sqrt is correctly rounded and monotonic, so s < t^2 (1 - 2^-40) (t^2 itself within 2^-53)
 // puts sqrt(s) below t (1 - 2^-42), which rounds below t, and s > t^2 (1 + 2^-40) puts it above; only between the
 // two (and for t <= 0, inf or NaN operands, where both comparisons fail) is the square root taken.
+// tt must be a normal double for its 2^-53 relative error (t^2 in the subnormal range has a far larger one, and the
+// 2^-40 margins would no longer hold): below DBL_MIN the square root decides.
 inline bool converged(V3 d, double t) {
     const double s = d.x * d.x + d.y * d.y + d.z * d.z;
-    if (t > 0.0) {
+    if (t > 0.0 && t * t >= 0x1p-1022) {
         const double tt = t * t;
         if (s < tt * (1.0 - 0x1p-40)) return true;
         if (s > tt * (1.0 + 0x1p-40)) return false;
@@ -249,7 +251,10 @@ std::unique_ptr<ScreenWs> alloc_ws() {
 }
 
 std::mutex g_ws_mu;
-std::unordered_map<const rt_ctx*, std::unique_ptr<ScreenWs>> g_ws;  // idle workspaces by context
+// Idle workspaces by context.  Allocated once and never destroyed: a context still alive at process exit leaks its
+// workspace instead of calling hipEventDestroy / hipHostFree / hipStreamDestroy from static destruction, after the
+// HIP runtime may have begun tearing down.
+auto& g_ws = *new std::unordered_map<const rt_ctx*, std::unique_ptr<ScreenWs>>();
 
 std::unique_ptr<ScreenWs> take_ws(const rt_ctx* ctx) {
     {
@@ -291,6 +296,19 @@ extern "C" int rt_render_screen(rt_ctx* ctx, const rt_scene* scene, const rt_cam
     if (depth < 0 || depth > RT_MAX_DEPTH) return rt_fail(RT_EINVAL, "rt_render_screen: depth out of range");
     if (rand_kind != RT_RAND_GLIBC && rand_kind != RT_RAND_MSVC)
         return rt_fail(RT_EINVAL, "rt_render_screen: unknown rand_kind");
+    // Everything below (the cached workspace's streams, events and mapped buffers, the trace launches) belongs to the
+    // context's device, whatever device the caller has current (rt_set_scene returns early for an unchanged scene
+    // without selecting it); the caller's device is restored on return.
+    struct DeviceGuard {
+        int prev = -1;
+        explicit DeviceGuard(int dev) {
+            if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+            (void)hipSetDevice(dev);
+        }
+        ~DeviceGuard() {
+            if (prev >= 0) (void)hipSetDevice(prev);
+        }
+    } device_guard(rt_ctx_device(ctx));
     int rc = rt_set_scene(ctx, scene);
     if (rc) return rc;
 

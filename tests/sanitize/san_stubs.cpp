@@ -30,6 +30,11 @@ hipError_t hipStreamDestroy(hipStream_t s) {
     return hipSuccess;
 }
 hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipGetDevice(int* d) {
+    *d = 0;
+    return hipSuccess;
+}
+hipError_t hipSetDevice(int) { return hipSuccess; }
 hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned int) {
     *e = reinterpret_cast<hipEvent_t>(new int(0));
     return hipSuccess;
@@ -73,6 +78,7 @@ struct rt_ctx {
     std::vector<unsigned char> blob;
 };
 
+int rt_ctx_device(const rt_ctx* c) { return c ? 0 : -1; }
 extern "C" int rt_ctx_create(int, rt_ctx** out) {
     *out = new rt_ctx();
     return RT_OK;

@@ -102,3 +102,20 @@ def test_run_ranks_terminates_blocked_peer(capsys):
 def test_run_ranks_no_line_is_failure(capsys):
     rc = bench.run_ranks(_fake_ranks(["pass", "pass"]), sys.stdout)
     assert rc == 1
+
+
+def test_c4_scaling_keys():
+    """The c4 leg's speed-up is against the same job's one-GPU c3 frame, never the group's own N = 1 figure."""
+    W, H, rays = 3840, 2160, 18_956_255
+    k = bench.c4_scaling_keys(8, W, H, rays, c4_ms=0.020, c3_ms_inflight=0.1265, c3_ms_serial=0.128)
+    assert k["speedup_vs_c3_1gpu"] == round(0.1265 / 0.020, 3)
+    assert k["efficiency"] == round(0.1265 / 0.020 / 8, 3)
+    assert k["speedup_vs_c3_1gpu_serial"] == round(0.128 / 0.020, 3)
+    assert k["mray_s_per_gpu"] == round(rays / 20e-6 / 1e6 / 8, 3)
+    assert k["hbm_write_frac_per_gpu"] == round(W * H * 4 / 8 / 20e-6 / 8e12, 5)
+    assert k["c3_1gpu_ms_per_frame"] == 0.1265
+    # a leg that did not time anything carries the baseline only
+    assert "speedup_vs_c3_1gpu" not in bench.c4_scaling_keys(8, W, H, rays, None, 0.1265, 0.128)
+    txt = bench.c4_parallelism_text(8, dict(k, value=947.8))
+    assert "8 GPUs" in txt and "efficiency" in txt and str(k["speedup_vs_c3_1gpu"]) in txt
+    assert bench.c4_parallelism_text(8, {"error": "x"}) == ""

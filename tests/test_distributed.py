@@ -5,6 +5,7 @@ no GPU — into a padded slab; the slabs go to rank 0 with the same gather_slabs
 (RCCL there, gloo here) and rank 0 puts the rows back with the C ABI's row map (rt_global_row).  The
 assembled frame must equal the single-process frame bit for bit.
 """
+import ctypes
 import os
 import socket
 
@@ -118,3 +119,193 @@ def test_auto_band_height_balances_bench_sizes():
             assert p.balanced, (H, N, p.band_height)
             assert sum(p.frame_local) == H and p.local[0] == N * p.frame_local[0]
     assert 1080 % (auto_band_height(1080, 8) * 8) == 0
+
+
+# ---- the product's group protocol (rt_group_plan.cpp), driven from real processes without a GPU -------------------
+# rt_render_multi's host decisions — what each rank sends, where rank 0's receives land, and the scene agreement —
+# are the C ABI functions below; here two (or three) gloo processes run them on their own scenes, exchange the votes
+# and the real packed slabs with exactly the byte counts the plan gives, and rank 0 assembles the frame.
+
+def _u64(words):
+    return (ctypes.c_uint64 * 4)(*[int(w) for w in words])
+
+
+def _pack_wire(rgb, fmt):
+    """The wire image of an oracle slab (rows x W x 3 f64), as the render kernel's packed stores write it."""
+    if fmt == 4:                                                   # GRAY8: the R byte of RGBA8
+        return np.floor(np.clip(rgb[..., 0], 0.0, 1.0) * 255.0 + 0.5).astype(np.uint8)
+    if fmt == 3:                                                   # RGB8
+        return np.floor(np.clip(rgb, 0.0, 1.0) * 255.0 + 0.5).astype(np.uint8)
+    if fmt == 1:                                                   # GRAY32F
+        return rgb[..., 0].astype(np.float32)
+    if fmt == 0:                                                   # RGBA32F
+        out = np.ones(rgb.shape[:-1] + (4,), np.float32)
+        out[..., :3] = rgb.astype(np.float32)
+        return out
+    raise AssertionError(fmt)
+
+
+def _protocol_worker(rank, world, port, W, H, scene_names, outputs, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import pyoracle as po
+        from ray_tracer_fragment_shader_amd import abi, scenes
+
+        L = abi.lib()
+        cfg = scenes.CONFIGS[scene_names[rank]] if scene_names[rank] in scenes.CONFIGS else None
+        scene = cfg.scene() if cfg else _chromatic_scene()
+        s_abi = scene.to_abi()
+        fp, achro = ctypes.c_uint64(), ctypes.c_int()
+        abi.check(L.rt_scene_fingerprint(ctypes.byref(s_abi), ctypes.byref(fp)), "rt_scene_fingerprint")
+        abi.check(L.rt_scene_achromatic(ctypes.byref(s_abi), ctypes.byref(achro)), "rt_scene_achromatic")
+        # --- the agreement: every rank votes before its first frame; the votes combine as ncclMax would
+        assert L.rt_group_agree_due(fp.value, 0, 0) == 1
+        vote = (ctypes.c_uint64 * 4)()
+        L.rt_group_agree_vote(fp.value, achro.value, vote)
+        mine = torch.from_numpy(np.array(list(vote), np.uint64).view(np.int64).copy())
+        votes = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(votes, mine)
+        acc = _u64(votes[0].numpy().view(np.uint64))
+        for v in votes[1:]:
+            L.rt_group_agree_combine(acc, _u64(v.numpy().view(np.uint64)))
+        verdict = L.rt_group_agree_verdict(acc)
+        result = {"verdict": verdict, "fp": fp.value}
+        if verdict != abi.RT_OK:
+            np.save(f"{out_path}_{rank}.npy", np.array([verdict], np.int64))
+            dist.barrier()
+            return
+        # once agreed, the same scene is not voted on again — also after an X -> Y -> X round trip on one rank
+        assert L.rt_group_agree_due(fp.value, 1, fp.value) == 0
+        assert L.rt_group_agree_due(fp.value ^ 1, 1, fp.value) == 1
+        # --- the frame plan: this rank's slab, sends, and (rank 0) receive table
+        plan = abi.rt_group_plan()
+        abi.check(L.rt_group_plan_frame(W, H, world, rank, 0, outputs, achro.value, ctypes.byref(plan)),
+                  "rt_group_plan_frame")
+        sends = torch.tensor([int(plan.send_bytes[0]), int(plan.send_bytes[1])], dtype=torch.int64)
+        all_sends = [torch.empty_like(sends) for _ in range(world)]
+        dist.all_gather(all_sends, sends)
+        rows = abi.rt_rows(plan.band_height, world, rank, 1)
+        rgb, _ = po.render(s_abi, cfg.camera(W, H) if cfg else scenes.CONFIGS["c2"].camera(W, H), W, H,
+                           cfg.depth if cfg else 1, rows=rows, nthreads=1)
+        assert rgb.shape[0] == plan.rank_rows
+        kinds = [k for k in range(2) if plan.wire[k] >= 0]
+        if rank == 0:
+            assert plan.send_bytes[0] == plan.send_bytes[1] == 0      # rank 0's slab is unpacked in place
+            gathered = {k: np.zeros(int(plan.gather_bytes[k]), np.uint8) for k in kinds}
+            total = 0
+            for q in range(1, world):
+                for k in kinds:
+                    off, nb = ctypes.c_uint64(), ctypes.c_uint64()
+                    abi.check(L.rt_group_plan_recv(ctypes.byref(plan), W, H, q, k, ctypes.byref(off),
+                                                   ctypes.byref(nb)), "rt_group_plan_recv")
+                    # both sides of every send / recv carry the same byte count
+                    assert nb.value == int(all_sends[q][k]), (q, k, nb.value, int(all_sends[q][k]))
+                    assert off.value + nb.value <= plan.gather_bytes[k] and off.value >= plan.slab_bytes[k] * q
+                    buf = torch.empty(nb.value, dtype=torch.uint8)
+                    dist.recv(buf, src=q)
+                    gathered[k][off.value: off.value + nb.value] = buf.numpy()
+                    total += nb.value
+            assert total == plan.payload_bytes
+            # rank 0's own rows from its slab; peers' from their slots; image rows by the C ABI's row map
+            img = {}
+            for k in kinds:
+                eb = plan.elem_bytes[k]
+                own = np.ascontiguousarray(_pack_wire(rgb, plan.wire[k])).view(np.uint8).reshape(-1)
+                slot = gathered[k].reshape(world, int(plan.slab_bytes[k]))
+                slot[0, : own.size] = own
+                out = np.zeros((H, W * eb), np.uint8)
+                for q in range(world):
+                    rq = abi.rt_rows(plan.band_height, world, q, 1)
+                    nl = ctypes.c_int()
+                    abi.check(L.rt_local_rows(H, ctypes.byref(rq), ctypes.byref(nl)), "rt_local_rows")
+                    for lr in range(nl.value):
+                        j = ctypes.c_int()
+                        abi.check(L.rt_global_row(H, ctypes.byref(rq), lr, ctypes.byref(j)), "rt_global_row")
+                        out[j.value] = slot[q, lr * W * eb: (lr + 1) * W * eb]
+                img[k] = out
+            np.savez(f"{out_path}_0.npz", **{f"k{k}": img[k] for k in kinds},
+                     wire=np.array([plan.wire[0], plan.wire[1]]), payload=np.array([plan.payload_bytes]))
+        else:
+            for k in kinds:
+                data = np.ascontiguousarray(_pack_wire(rgb, plan.wire[k])).view(np.uint8).reshape(-1)
+                assert data.size == plan.send_bytes[k] and plan.slab_bytes[k] >= data.size
+                dist.send(torch.from_numpy(data.copy()), dst=0)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _chromatic_scene():
+    """The c2 scene with a reddish light: R != G, so the wire formats are RGB8 / RGBA32F."""
+    from ray_tracer_fragment_shader_amd import scenes
+    sc = scenes.CONFIGS["c2"].scene()
+    sc.lights[0].color = (1.0, 0.5, 0.25)
+    return sc
+
+
+@pytest.mark.parametrize("world,names,outputs", [
+    (2, ("c2", "c2"), 3),            # achromatic: GRAY32F + GRAY8
+    (3, ("chroma",) * 3, 2),         # chromatic, RGBA8 only: RGB8
+])
+def test_group_protocol_plan_and_gather(tmp_path, world, names, outputs):
+    from oracle import pyoracle as po
+    from ray_tracer_fragment_shader_amd import abi, scenes
+
+    W, H = 72, 50
+    prefix = str(tmp_path / "proto")
+    mp.spawn(_protocol_worker, args=(world, _free_port(), W, H, names, outputs, prefix), nprocs=world, join=True)
+    got = np.load(f"{prefix}_0.npz")
+    cfg = scenes.CONFIGS["c2"]
+    scene = cfg.scene() if names[0] in scenes.CONFIGS else _chromatic_scene()
+    want, _ = po.render(scene.to_abi(), cfg.camera(W, H), W, H, cfg.depth)
+    for k in range(2):
+        if f"k{k}" not in got:
+            assert not outputs & (1 << k)
+            continue
+        fmt = int(got["wire"][k])
+        assert fmt == ({0: abi.RT_PIXEL_GRAY32F, 1: abi.RT_PIXEL_GRAY8} if names[0] == "c2"
+                       else {0: abi.RT_PIXEL_RGBA32F, 1: abi.RT_PIXEL_RGB8})[k]
+        ref = np.ascontiguousarray(_pack_wire(want, fmt)).view(np.uint8).reshape(H, -1)
+        assert np.array_equal(got[f"k{k}"], ref)
+
+
+def test_group_protocol_scene_mismatch_fails_on_every_rank(tmp_path):
+    """Ranks holding different scenes: the combined votes fail the verdict with RT_EINVAL on every rank (before
+    any slab is sent), instead of mismatched send / receive sizes."""
+    from ray_tracer_fragment_shader_amd import abi
+    prefix = str(tmp_path / "mismatch")
+    mp.spawn(_protocol_worker, args=(2, _free_port(), 40, 30, ("c2", "c3"), 3, prefix), nprocs=2, join=True)
+    for r in range(2):
+        assert int(np.load(f"{prefix}_{r}.npy")[0]) == abi.RT_EINVAL
+
+
+def test_group_plan_matches_band_plan():
+    """rt_group_plan_frame against the band plan and pixel sizes it is built from, for the bench sizes."""
+    from ray_tracer_fragment_shader_amd import abi
+    L = abi.lib()
+    for W, H in ((1920, 1080), (3840, 2160), (7680, 4320), (97, 61)):
+        for n in (1, 2, 3, 8):
+            for achro in (0, 1):
+                plans = []
+                for r in range(n):
+                    p = abi.rt_group_plan()
+                    abi.check(L.rt_group_plan_frame(W, H, n, r, 0, 3, achro, ctypes.byref(p)), "plan")
+                    plans.append(p)
+                hb, slab = ctypes.c_int(), ctypes.c_int()
+                abi.check(L.rt_band_plan(H, n, 0, ctypes.byref(hb), ctypes.byref(slab)), "rt_band_plan")
+                assert all(p.band_height == hb.value and p.slab_rows == slab.value for p in plans)
+                assert sum(p.rank_rows for p in plans) == H
+                eb = (4, 1) if achro else (16, 3)
+                for k in range(2):
+                    assert all(p.elem_bytes[k] == eb[k] and p.slab_bytes[k] == slab.value * W * eb[k] for p in plans)
+                    assert sum(p.send_bytes[k] for p in plans) == (H - plans[0].rank_rows) * W * eb[k] * (n > 1)
+                assert plans[0].payload_bytes == sum(p.send_bytes[0] + p.send_bytes[1] for p in plans[1:])
+                if n > 1:
+                    assert plans[0].gather_bytes[1] == n * plans[0].slab_bytes[1]
+    # misuse: a receive table asked of a rank other than 0, or of a peer out of range
+    p = abi.rt_group_plan()
+    abi.check(L.rt_group_plan_frame(64, 64, 2, 1, 0, 3, 1, ctypes.byref(p)), "plan")
+    off, nb = ctypes.c_uint64(), ctypes.c_uint64()
+    assert L.rt_group_plan_recv(ctypes.byref(p), 64, 64, 1, 0, ctypes.byref(off), ctypes.byref(nb)) == abi.RT_EINVAL

@@ -473,6 +473,26 @@ def test_render_screen_faithful_vs_oracle(tr, name, W, H, rng, seed):
             assert calls == g["calls"]
 
 
+def test_render_screen_on_another_device_than_current():
+    """rt_render_screen on a context of device 1 while device 0 is current: its workspace (streams, events, mapped
+    buffers) and launches belong to the context's device, the frame equals the restatement, and the caller's current
+    device is unchanged afterwards."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    t1 = Tracer(1)
+    try:
+        sc = scenes.CONFIGS["demo"].scene()
+        for _ in range(2):                                  # the second call reuses the cached workspace
+            torch.cuda.set_device(0)
+            rgb, _, ns, calls = _render_screen(t1, sc, 64, 48, 5, 0, 1)
+            assert torch.cuda.current_device() == 0
+            want_rgb, want_ns, want_calls = po.render_screen(sc.to_abi(), 64, 48, 5, 0, 1)
+            assert np.array_equal(ns, want_ns) and calls == want_calls and np.array_equal(rgb, want_rgb)
+    finally:
+        t1.close()
+
+
 @pytest.mark.parametrize("env", [{"RT_SCREEN_NEXT_MIN": "0"}, {"RT_SCREEN_NEXT_MIN": "0", "RT_SCREEN_AHEAD": "2"},
                                  {"RT_SCREEN_NEXT": "0"}, {"RT_SCREEN_NEXT_MIN": "0", "RT_SCREEN_PROGRESSIVE": "1"}],
                          ids=["every_chunk", "ahead2", "next0", "progressive"])

@@ -1,0 +1,73 @@
+#!/bin/bash
+# Round-5 GPU session.  STEPS selects parts (default: tests bench); each GPU step has its own time limit and the
+# script stops at the first failure.
+#   tests     pytest -m gpu
+#   bench     the default bench line (N = 1)
+#   rehearse  bench.py --gpus 2 --backend gloo (two ranks sharing the GPU; the c4 leg as a COPY group on rank 0)
+#   trace     per-wave timeline of one c2 / c5 launch (tools/_var/trace, RT_WAVE_TRACE=2 build) with the attribution
+#   c4n1      tools/c4_n1_probe.py: the one-rank rt_render_multi frame against plain c3 renders
+#   ab        tools/ab_libs.py over tools/_var/* (VARS=comma list, CONFIGS, ROUNDS; INFLIGHT for the bench pattern)
+#   prof      one-stream rocprofv3 kernel-trace summaries at c2 / c3 / c5 (CONFIGS)
+#   pmc       PMC passes per config (tools/pmc.sh)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+want() { case " ${STEPS:-tests bench} " in *" $1 "*) return 0;; esac; return 1; }
+LIB=ray_tracer_fragment_shader_amd/lib/librt_amd.so
+if want tests; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} \
+      > "$OUT/gpu_tests.log" 2>&1
+  rc=$?; tail -5 "$OUT/gpu_tests.log"; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit $rc; }
+fi
+if want trace; then
+  cp "$LIB" /tmp/librt_amd.base.so
+  cp tools/_var/trace/librt_amd.so "$LIB"
+  for c in ${TRACE_CONFIGS:-c2}; do
+    timeout -k 10 120 python -u tools/wave_trace.py $c > "$OUT/wave_trace_$c.json" 2> "$OUT/wave_trace_$c.err"
+    rc=$?
+    [ $rc -eq 0 ] || { cp /tmp/librt_amd.base.so "$LIB"; echo "wave trace $c rc=$rc"; tail -20 "$OUT/wave_trace_$c.err"; exit 20; }
+    python3 -c "import json; d=json.load(open('$OUT/wave_trace_$c.json')); print('$c', d['span_us'], d.get('attribution_us'), d.get('mean_phase_us'), d.get('resident_max'))"
+  done
+  cp /tmp/librt_amd.base.so "$LIB"
+fi
+if want c4n1; then
+  timeout -k 10 180 python -u tools/c4_n1_probe.py > "$OUT/c4_n1.json" 2> "$OUT/c4_n1.err" \
+      || { echo "c4_n1 probe failed"; tail -20 "$OUT/c4_n1.err"; exit 21; }
+  cat "$OUT/c4_n1.json"
+fi
+if want ab; then
+  VARS=${VARS:-} timeout -k 10 ${AB_TIMEOUT:-600} python -u tools/ab_libs.py ${CONFIGS:-c2,c3,c5} ${ROUNDS:-9} \
+      > "$OUT/ab.jsonl" 2> "$OUT/ab.err" || { echo "ab failed"; tail -20 "$OUT/ab.err"; exit 22; }
+  cat "$OUT/ab.jsonl"
+fi
+if want bench; then
+  timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" \
+      || { echo "bench failed"; tail -30 "$OUT/bench.err"; exit 3; }
+  python3 -c "import json; d=json.load(open('$OUT/bench.json')); r=d['roofline']; print(d['value'], d['ms_per_step'], r['kernel_ms_serial'], r['interval_ms_in_flight'], {k: v.get('kernel_ms_serial') for k, v in d.get('configs', {}).items()}, json.dumps(d.get('c4', {}))[:1200], json.dumps(d.get('drop_in', {}))[:900])"
+fi
+if want rehearse; then
+  timeout -k 10 600 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-cpu-baseline \
+      > "$OUT/rehearse.json" 2> "$OUT/rehearse.err" || { echo "rehearsal failed"; tail -30 "$OUT/rehearse.err"; exit 4; }
+  python3 -c "import json; d=json.load(open('$OUT/rehearse.json')); print(d['n_gpus'], d['value'], d['config']['parallelism']); print(json.dumps(d.get('c4'))[:1500])"
+fi
+if want prof; then
+  cd /tmp && export TMPDIR=/tmp
+  for c in ${CONFIGS:-c2 c3 c5}; do
+    steps=100; [ "$c" = "c5" ] && steps=30
+    rm -rf "$OUT/prof1_$c"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof1_$c" -o run -- \
+        python3 "$ROOT/bench.py" --config $c --steps $steps --warmup 5 --no-cpu-baseline --profile-kernel-only \
+        --frames-in-flight 1 > "$OUT/prof1_bench_$c.json" 2> "$OUT/prof1_$c.err" \
+        || { echo "rocprof $c failed"; tail -20 "$OUT/prof1_$c.err"; exit 5; }
+    echo "== $c"; find "$OUT/prof1_$c" -name "*kernel_stats.csv" -exec head -3 {} \;
+  done
+  cd "$ROOT"
+fi
+if want pmc; then
+  for c in ${CONFIGS:-c2 c3 c5}; do
+    CONFIG=$c timeout -k 10 900 bash tools/pmc.sh > "$OUT/pmc_$c.log" 2>&1 || { echo "pmc $c failed"; tail -20 "$OUT/pmc_$c.log"; exit 6; }
+    tail -2 "$OUT/pmc_$c.log"
+  done
+fi

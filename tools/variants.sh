@@ -6,7 +6,7 @@ set -eu
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 SRC=$ROOT/ray_tracer_fragment_shader_amd/csrc
 LIB=$ROOT/ray_tracer_fragment_shader_amd/lib
-make -C "$SRC" -s ../lib/rt_host.o ../lib/rt_screen.o ../lib/rt_group.o
+make -C "$SRC" -s ../lib/rt_host.o ../lib/rt_screen.o ../lib/rt_group.o ../lib/rt_group_plan.o
 UNITS="rt_kernel rt_render_b0 rt_render_b1 rt_render_b2 rt_render_b3 rt_render_b4 rt_render_b5 rt_render_b6 rt_render_b7"
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
@@ -15,7 +15,7 @@ for spec in "$@"; do
       -fno-fast-math -Wall -Wno-unused-function --offload-arch=gfx950 -DRT_MAX_B=${RT_MAX_B:-3} $flags -c {}.hip -o "$d/{}.o")
   objs=$(for u in $UNITS; do echo "$d/$u.o"; done)
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$d/librt_amd.so" $objs "$LIB/rt_host.o" "$LIB/rt_screen.o" \
-      "$LIB/rt_group.o" -L/opt/rocm/lib -lrccl
+      "$LIB/rt_group.o" "$LIB/rt_group_plan.o" -L/opt/rocm/lib -lrccl
   rm -f $objs
   echo "built $name"
 done
