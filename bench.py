@@ -29,6 +29,7 @@ Extra legs in the same JSON line (outside the timed region of `value`):
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys

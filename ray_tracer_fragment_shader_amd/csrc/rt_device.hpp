@@ -97,6 +97,18 @@
 // c3 (depth 2) -1.2 to -1.9%, c2 (depth 1) +0.7 to +1.1% (r02, in-process A/B) — hence depth >= 2 until r04.  The
 // 7-wave depth-1 kernel (94 SGPRs, 65 VGPRs, no scratch) gains from them: c2 -1.9% serial, -0.5% with 3 frames
 // in flight (r04, in-process A/B; the skips alone -1.4%, the parking alone +0.8%) — hence depth >= 1.
+// 1: closest-hit distances are computed only when two candidates meet (take_closer).
+#ifndef RT_LAZY_DIST
+#define RT_LAZY_DIST 1
+#endif
+// 1: primary rays that hit an object skip the bounding-sphere cull when the eye's per-eye flag proves they pass it.
+#ifndef RT_PRIM_BOUND_SKIP
+#define RT_PRIM_BOUND_SKIP 1
+#endif
+// 1: the reference's board is decided by the hit point's position in its square where that is certain (board_hit).
+#ifndef RT_BOARD_POS
+#define RT_BOARD_POS 1
+#endif
 // 1: primary rays of waves whose cone mask keeps no sphere normalise their direction only where they hit the board.
 #ifndef RT_LAZY_PRIMARY_U
 #define RT_LAZY_PRIMARY_U 1
@@ -411,6 +423,29 @@ __device__ __forceinline__ bool board_hit(const DevScene* S, d3 p0, d3 d, d3* p)
     if (m < S->eps) return false;                           // :659
     d3 q = add(p0, scl(m, d));                              // :665
     d3 w = sub(q, v0);                                      // :667
+#if RT_BOARD_POS
+    // The reference's board (host: board_fast) decided by the position of w in its square, where that is certain.
+    // With L the side, T1 = (P1, P2, P3) and T2 = (P1, P3, P4) give, in exact arithmetic on the computed w,
+    //   T1: s = (wx - wz) / L, t = wz / L;   T2: s = wx / L, t = (wz - wx) / L
+    // (uu, uv, vv, den are exact for an integer L <= 2^12, the products with u's and v's zero components vanish),
+    // and the reference's rounded s, t (:670-674) err by less than E = 64 u (|wx| + |wz|) / L + 4 u (u = 2^-53: two
+    // roundings per dot product, three in A and B, one quotient).  For |wx|, |wz| <= far = 2^24 L, E < 2^-22 + 2^-51;
+    // the margin delta = L 2^-19 keeps every decision below at least delta / (2L) = 2^-20 > 2E + u |s + t| away:
+    //  * delta <= wx, wz <= L - delta and |wx - wz| >= delta: the triangle on w's side of the diagonal has
+    //    s, t >= delta / L and s + t <= 1 - delta / L — it passes (:676), a hit at q;
+    //  * wx <= -delta, wz <= -delta, wx >= L + delta or wz >= L + delta: each triangle fails one of its three tests
+    //    by >= delta / (2L) (e.g. wx <= -delta: T2's s < 0, and T1's s + t = wx / L < 0 puts s or t below -delta/(2L)).
+    // Everything else — within delta of an edge or the diagonal, |w| beyond `far`, NaN — takes the exact tests.
+    if (S->board_fast) {
+        const double wx = w.x, wz = w.z, lo = S->board_lo, hi = S->board_hi, diag = fabs(wx - wz);
+        if ((wx >= lo) & (wz >= lo) & (wx <= hi) & (wz <= hi) & (diag >= lo)) {
+            *p = q;
+            return true;
+        }
+        const double far = S->board_far, out = S->board_out, ax = fabs(wx), az = fabs(wz);
+        if ((ax <= far) & (az <= far) & ((wx <= -lo) | (wz <= -lo) | (wx >= out) | (wz >= out))) return false;
+    }
+#endif
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         const DevTri& Tt = S->tri[t];
@@ -548,7 +583,9 @@ __device__ __forceinline__ void meshes_closest(const SceneView& V, const Ray& r,
         d3 mq;
         int t = mesh_closest_tri(V, M, r.p0, r.d, eps, &mbest, &mq);
         if (t < 0) continue;
-        if (mbest < *best || *best < 0.0 || (mbest == *best && M.child < child_of(V, *kind))) {
+        // (a deferred distance of the current candidate, take_closer, is computed here)
+        if (RT_LAZY_DIST && *kind >= 0 && *best < 0.0) *best = len_fast(sub(*hp, r.p0));
+        if (mbest < *best || *kind < 0 || (mbest == *best && M.child < child_of(V, *kind))) {
             *best = mbest;
             *kind = kMeshKind + 16 * m + (t - M.tri0);
             *hp = mq;
@@ -593,6 +630,36 @@ __device__ __forceinline__ bool sphere_hit(const DevSphere& sp, d3 p0, d3 u, dou
 // Bits of the spheres a 64-bit mask may name: k < min(np, 64).
 __device__ __forceinline__ uint64_t sphere_bits(int np) { return np >= 64 ? ~0ull : ((1ull << np) - 1); }
 
+// The closest-hit update (:811-818) for candidate q of kind k: the reference keeps the first candidate and then
+// one with a strictly smaller Euclidean distance |q - p0|.  Distances are compared only when two candidates meet,
+// so they are computed only then (RT_LAZY_DIST): the first candidate's is deferred — *best < 0 with *kind >= 0
+// means "not computed yet" — and a ray with a single candidate (most board and sphere hits) computes none.  The
+// same comparisons on the same values: kind and hit point are unchanged, bit for bit (a NaN distance compares false
+// either way, and a computed NaN best is never recomputed: NaN < 0 is false).
+__device__ __forceinline__ void take_closer(d3 p0, d3 q, int k, int* kind, double* best, d3* hp) {
+#if RT_LAZY_DIST
+    if (*kind < 0) {
+        *kind = k;
+        *hp = q;
+        return;
+    }
+    if (*best < 0.0) *best = len_fast(sub(*hp, p0));
+    const double dist = len_fast(sub(q, p0));                // :811-812
+    if (dist < *best) {                                      // :813
+        *best = dist;
+        *kind = k;
+        *hp = q;
+    }
+#else
+    const double dist = len_fast(sub(q, p0));
+    if (dist < *best || *best < 0.0) {
+        *best = dist;
+        *kind = k;
+        *hp = q;
+    }
+#endif
+}
+
 // Closest hit of g_scene (:796-821): Euclidean distance |p - p0|, strict <, board (child 0) first.
 // kind: -1 miss, 0 board, 1 + k sphere k.
 // Spheres go in batches of kChunk: the FP32 filter of the whole batch is evaluated branch-free (records
@@ -622,14 +689,7 @@ __device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const R
 #if RT_SEC_PREFETCH
         {
             d3 q;
-            if (sphere_hit(sp4[j], r.p0, r.u, eps, &q)) {
-                double dist = len_fast(sub(q, r.p0));            // :811-812
-                if (dist < *best || *best < 0.0) {          // :813
-                    *best = dist;
-                    *kind = 1 + k;
-                    *hp = q;
-                }
-            }
+            if (sphere_hit(sp4[j], r.p0, r.u, eps, &q)) take_closer(r.p0, q, 1 + k, kind, best, hp);
             continue;
         }
 #endif
@@ -639,14 +699,7 @@ __device__ __forceinline__ void sphere_batch_closest(const SceneView& V, const R
         pass &= pass - 1;
 #endif
         d3 q;
-        if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) {
-            double dist = len_fast(sub(q, r.p0));                // :811-812
-            if (dist < *best || *best < 0.0) {              // :813
-                *best = dist;
-                *kind = 1 + k;
-                *hp = q;
-            }
-        }
+        if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) take_closer(r.p0, q, 1 + k, kind, best, hp);   // :811-813
     }
 }
 
@@ -663,11 +716,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
     double best = -1.0;
     if (S->has_board && skip != 0) {
         d3 q;
-        if (board_hit(S, r.p0, r.d, &q)) {
-            kind = 0;
-            best = len_fast(sub(q, r.p0));
-            *hp = q;
-        }
+        if (board_hit(S, r.p0, r.d, &q)) take_closer(r.p0, q, 0, &kind, &best, hp);
     }
     const double eps = S->eps;
     int k0 = 0;
@@ -687,14 +736,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
 #endif
             RT_COUNT(S, kCntExactRay, 1);
             d3 q;
-            if (sphere_hit(sp, r.p0, r.u, eps, &q)) {
-                double dist = len_fast(sub(q, r.p0));       // :811-812
-                if (dist < best || best < 0.0) {            // :813
-                    best = dist;
-                    kind = 1 + k;
-                    *hp = q;
-                }
-            }
+            if (sphere_hit(sp, r.p0, r.u, eps, &q)) take_closer(r.p0, q, 1 + k, &kind, &best, hp);   // :811-813
         }
         k0 = 64;
     }
@@ -731,14 +773,7 @@ __device__ __forceinline__ void primary_sphere(const SceneView& V, const Ray& r,
 #endif
     d3 q;
     RT_COUNT(V.S, kCntExactPrimary, 1);
-    if (sphere_hit_dp(ld3(pp.dP), pp.dd, r2, r.p0, r.u, eps, &q)) {
-        double dist = len_fast(sub(q, r.p0));
-        if (dist < *best || *best < 0.0) {
-            *best = dist;
-            *kind = 1 + k;
-            *hp = q;
-        }
-    }
+    if (sphere_hit_dp(ld3(pp.dP), pp.dd, r2, r.p0, r.u, eps, &q)) take_closer(r.p0, q, 1 + k, kind, best, hp);
 }
 
 // Closest hit of a primary ray Line(eye, sp): deltaP and |deltaP|^2 per sphere were computed for this
@@ -758,11 +793,7 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, Ray& r, u
     double best = -1.0;
     if (S->has_board) {
         d3 q;
-        if (board_hit<true>(S, r.p0, r.d, &q)) {
-            kind = 0;
-            best = len_fast(sub(q, r.p0));
-            *hp = q;
-        }
+        if (board_hit<true>(S, r.p0, r.d, &q)) take_closer(r.p0, q, 0, &kind, &best, hp);
     }
     const double eps = S->eps;
     int k0 = 0;
@@ -793,14 +824,7 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, Ray& r, u
 #endif
             const DevSpherePrim& pp = V.prim[k];
             d3 q;
-            if (sphere_hit_dp(ld3(pp.dP), pp.dd, V.sph[k].r2, r.p0, r.u, eps, &q)) {
-                double dist = len_fast(sub(q, r.p0));
-                if (dist < best || best < 0.0) {
-                    best = dist;
-                    kind = 1 + k;
-                    *hp = q;
-                }
-            }
+            if (sphere_hit_dp(ld3(pp.dP), pp.dd, V.sph[k].r2, r.p0, r.u, eps, &q)) take_closer(r.p0, q, 1 + k, &kind, &best, hp);
         }
     }
     if (FULL) meshes_closest(V, r, eps, &kind, &best, hp);
@@ -808,7 +832,8 @@ __device__ __forceinline__ int closest_hit_primary(const SceneView& V, Ray& r, u
     // The bounding-sphere cull (:747-758) only turns hits into misses, so it is evaluated last and only
     // for rays that hit something: waves of background rays skip it.
     // (deltaP = bc - eye, computed here for the waves that need it rather than held from the kernel's start)
-    if (kind >= 0) {
+    // (prim_bound_ok, per eye: every primary hit passes it — proof at rt_prepare_kernel)
+    if (kind >= 0 && !(RT_PRIM_BOUND_SKIP && S->prim_bound_ok)) {
         const d3 bdP = sub(ld3(S->bc), r.p0);               // :740 with p0 = camera
         if (!bound_pass_dp(S, bdP, dot(bdP, bdP), r.u)) kind = -1;
     }

@@ -421,6 +421,31 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
         const double y = (eps2 / 2 / 0x1p-50 - 5 * std::fabs(d->tri[0].v0[1]) - 1) / 3;
         if (y > 0 && std::isfinite(y)) d->board_skip_y = y;
     }
+    // Board decided by position (rt_device.hpp board_hit): the reference's CheckerBoard exactly — normal (0, -1, 0),
+    // T1 = (P1, P2, P3) with u = (L, 0, 0), v = (L, 0, L), T2 = (P1, P3, P4) with u = (L, 0, L), v = (0, 0, L) — and an
+    // integer side L <= 2^12, so uu, uv, vv and den are exact.  Margin delta = L 2^-19, range far = 2^24 L (proof at
+    // board_hit).
+    d->board_fast = 0;
+    d->board_lo = d->board_hi = d->board_out = inf;
+    d->board_far = -1.0;
+    if (d->has_board) {
+        const rt::DevTri &T1 = d->tri[0], &T2 = d->tri[1];
+        const double L = 2 * s->board_half_size;
+        auto is3 = [](const double* a, double x, double y, double z) { return a[0] == x && a[1] == y && a[2] == z; };
+        const bool shape = L >= 1 && L <= 4096 && L == std::floor(L) && is3(T1.n, 0, -1, 0) && is3(T2.n, 0, -1, 0) &&
+                           is3(T1.u, L, 0, 0) && is3(T1.v, L, 0, L) && is3(T2.u, L, 0, L) && is3(T2.v, 0, 0, L) &&
+                           is3(T1.v0, T2.v0[0], T2.v0[1], T2.v0[2]) && T1.uu == L * L && T1.uv == L * L &&
+                           T1.vv == 2 * L * L && T2.uu == 2 * L * L && T2.uv == L * L && T2.vv == L * L &&
+                           T1.den == -(L * L * L * L) && T2.den == -(L * L * L * L);
+        if (shape) {
+            const double delta = std::ldexp(L, -19);
+            d->board_fast = 1;
+            d->board_lo = delta;
+            d->board_hi = L - delta;
+            d->board_out = L + delta;
+            d->board_far = std::ldexp(L, 24);
+        }
+    }
     for (int m = 0; m < 5; ++m) d->mat[m] = dm[m];
     d->transparent = any_transparent ? 1 : 0;
     d->tree = tree ? 1 : 0;

@@ -104,6 +104,15 @@ __global__ __launch_bounds__(kThreads) void rt_prepare_kernel(DevScene* __restri
         // board plane numerator for p0 = eye, as board_hit computes it (:657)
         g->board_num = dot(ld3(g->tri[0].n), sub(ld3(g->tri[0].v0), eye));
         g->hits_ok = hits_ok_from(g, eye);      // hit points of rays from this eye skip the cull (hits_inside)
+        // A primary ray that hits an object passes g_scene's cull when every object lies within R - 1 of bc
+        // (hits_inside) and the eye is at least R + 1 away: the line then passes within R - 1 of bc, so its exact
+        // disc >= R^2 - (R - 1)^2 = 2R - 1, and the eye being outside the bound puts the entry root at
+        // s >= D - R >= 1 (the hit lies ahead of the eye, past the entry); the FP64 rounding of disc and s is
+        // ~2^-49 (D^2 + R^2) and ~2^-50 (D + R), far below 2R - 1 and 1 - eps for D <= 2^20 (R + 1).
+        const double bx = eye.x - g->bc[0], by = eye.y - g->bc[1], bz = eye.z - g->bc[2];
+        const double D2 = bx * bx + by * by + bz * bz, R1 = sqrt(g->br2) + 1.0;
+        g->prim_bound_ok = (g->bound_on != 0) & (g->hits_inside != 0) & (D2 >= R1 * R1 * (1.0 + 0x1p-30)) &
+                           (D2 <= R1 * R1 * 0x1p40);
     }
     if (k >= np) return;
     d3 dP = sub(ld3(sph[k].c), eye);

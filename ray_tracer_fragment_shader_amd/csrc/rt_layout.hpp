@@ -131,6 +131,9 @@ struct alignas(16) DevScene {
     double self_eps2;                  // eps^2 / 4: sphere self-test skip threshold (origin_skip)
     double hits_lim2;                  // hits_inside holds for rays whose level-0 origin o has |o - bc|^2 <= this
     double board_num;                  // n . (v0 - eye) of the board plane for the camera `eye` (per eye)
+    // Board decided by position (board_fast, rt_device.hpp board_hit): margin delta, L - delta, L + delta and the
+    // range |w| <= far within which the decisions' error bound holds (w = hit point - vertex 0, L = board side)
+    double board_lo, board_hi, board_out, board_far;
     double eye[3];                     // camera the *Prim arrays and board_num were computed for
     int32_t bound_on;                  // g_scene radius > 0
     int32_t has_board;
@@ -145,6 +148,8 @@ struct alignas(16) DevScene {
     int32_t tree;                      // some material transmits AND reflects: ray-tree kernels (trace_tree)
     int32_t hits_inside;               // every hit point lies within (R - 1) of bc: rays from hits pass the cull
     int32_t hits_ok;                   // hits_inside for the camera eye (rt_prepare_kernel, per eye)
+    int32_t board_fast;                // the reference's board, exactly: barycentric tests decided by position
+    int32_t prim_bound_ok;             // per eye: every primary ray that hits an object passes the cull (rt_prepare_kernel)
     unsigned long long* counters;      // RT_COUNTERS builds (tools/counters.py): per-wave event counters, else null
     DevTri tri[2];                     // board triangles T1 = (P1,P2,P3), T2 = (P1,P3,P4)   (:840-841)
     DevMat mat[5];                     // 0 white square, 1 black square, 2 sphere, 3 tetrahedron, 4 cube

@@ -106,6 +106,53 @@ def test_intersection_kat(tr, name):
         assert np.array_equal(got[f], k[f]), f
 
 
+def _board_edge_rays():
+    """Rays whose board-plane hit points sit at chosen offsets around the board's edges and its diagonal — both sides
+    of the position shortcut's margin delta = L 2^-19 (board_hit) — and far beyond the board (|w| up to 2^24 L and
+    past it), from the eye, from above the board and from grazing origins."""
+    L, v0 = 320.0, np.array([-160.0, 0.0, -320.0])
+    delta = L * 2.0 ** -19
+    offs = [0.0, 1e-13, -1e-13, 1e-7, -1e-7, delta / 2, -delta / 2, delta, -delta, 2 * delta, -2 * delta, 1e-2, -1e-2,
+            5.0, -5.0]
+    pts = []
+    for e in offs:
+        for a in (0.0, L):                                  # edges wx = 0, L and wz = 0, L
+            for b in (37.0, 160.0 + e / 3, L - 11.0):
+                pts += [(a + e, b), (b, a + e)]
+        for b in (1.0, 100.0, 250.0, L - 1.0):              # the diagonal wx = wz
+            pts += [(b + e, b), (b, b + e)]
+    for far in (1e6, 2.0 ** 24 * L * 0.999, 2.0 ** 24 * L * 1.001, 1e12):
+        pts += [(far, 100.0), (100.0, -far), (-far, -far)]
+    q = v0 + np.array([[wx, 0.0, wz] for wx, wz in pts])
+    starts, ends = [], []
+    for o in ((0.0, 100.0, 200.0), (10.0, 50.0, -100.0), (0.0, 3e6, -160.0), (-500.0, 0.5, -160.0)):
+        o = np.array(o)
+        for t in q:
+            starts.append(o)
+            ends.append(o + (t - o) * 0.5)                 # the plane is crossed at m = 2
+    return np.array(starts), np.array(ends)
+
+
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_board_position_shortcut_edges(tr, name):
+    """The board decided by its hit point's position (board_hit, RT_BOARD_POS) equals the reference's barycentric
+    tests on both sides of the margin, on the diagonal and far away: hits, points and colours, bit for bit."""
+    cfg = scenes.CONFIGS[name]
+    tr.set_scene(cfg.scene())
+    s, e = _board_edge_rays()
+    got = decode_hits(tr.intersect(torch.tensor(s, device="cuda"), torch.tensor(e, device="cuda")))
+    want = po.intersect(cfg.scene().to_abi(), s, e)
+    assert np.array_equal(got["hit"], want["hit"])
+    assert np.array_equal(got["material"], want["material"])
+    assert np.array_equal(got["point"], want["point"])
+    for depth in (0, 2):
+        rgb, _ = tr.trace_rays(torch.tensor(s, device="cuda"), torch.tensor(e, device="cuda"), depth)
+        want_rgb, _ = po.trace_rays(cfg.scene().to_abi(), s, e, depth)
+        assert np.array_equal(rgb.cpu().numpy(), want_rgb)
+    # both outcomes occur near every edge: the test exercises the exact fallback and the shortcut
+    assert 0 < int(np.sum(want["hit"])) < len(s)
+
+
 @pytest.mark.parametrize("name", ["c3", "c5", "demo"])
 def test_trace_rays_kat(tr, name):
     cfg = scenes.CONFIGS[name]

@@ -6,6 +6,8 @@
 #   rehearse  bench.py --gpus 2 --backend gloo (two ranks sharing the GPU; the c4 leg as a COPY group on rank 0)
 #   trace     per-wave timeline of one c2 / c5 launch (tools/_var/trace, RT_WAVE_TRACE=2 build) with the attribution
 #   c4n1      tools/c4_n1_probe.py: the one-rank rt_render_multi frame against plain c3 renders
+#   hostw     tools/_mb_hostwrite (kernel stores into pinned host memory by store shape)
+#   refill    tools/_var/mb_refill: traced wave durations replayed as sleeps, by LDS / VGPR footprint
 #   ab        tools/ab_libs.py over tools/_var/* (VARS=comma list, CONFIGS, ROUNDS; INFLIGHT for the bench pattern)
 #   prof      one-stream rocprofv3 kernel-trace summaries at c2 / c3 / c5 (CONFIGS)
 #   pmc       PMC passes per config (tools/pmc.sh)
@@ -36,6 +38,19 @@ if want c4n1; then
   timeout -k 10 180 python -u tools/c4_n1_probe.py > "$OUT/c4_n1.json" 2> "$OUT/c4_n1.err" \
       || { echo "c4_n1 probe failed"; tail -20 "$OUT/c4_n1.err"; exit 21; }
   cat "$OUT/c4_n1.json"
+fi
+if want hostw; then
+  timeout -k 10 120 ./tools/_mb_hostwrite > "$OUT/hostwrite.jsonl" 2> "$OUT/hostwrite.err" \
+      || { echo "hostwrite failed"; tail -20 "$OUT/hostwrite.err"; exit 23; }
+  cat "$OUT/hostwrite.jsonl"
+fi
+if want refill; then
+  for c in ${REFILL_CONFIGS:-c5 c2}; do
+    gx=960; [ "$c" = "c2" ] && gx=240
+    timeout -k 10 120 ./tools/_var/mb_refill $c $gx >> "$OUT/refill.jsonl" 2> "$OUT/refill.err" \
+        || { echo "refill $c failed"; tail -20 "$OUT/refill.err"; exit 24; }
+  done
+  cat "$OUT/refill.jsonl"
 fi
 if want ab; then
   VARS=${VARS:-} timeout -k 10 ${AB_TIMEOUT:-600} python -u tools/ab_libs.py ${CONFIGS:-c2,c3,c5} ${ROUNDS:-9} \
