@@ -915,7 +915,7 @@ def main() -> int:
         dog.start()
         try:
             c3 = scenes.CONFIGS["c3"]
-            steps4 = max(10, min(args.steps, 40))
+            steps4 = 40                                    # (fixed: the first launch and the final sync weigh less)
             # the denominator of the split frame's speed-up: the same job's one-GPU c3 frame (same scene, view and
             # RGBA8 output), measured on rank 0 before the group leg at every N
             base = (c3_one_gpu(torch, L, abi, Tracer, c3, dev, local, max(1, args.frames_in_flight), steps4)

@@ -8,6 +8,8 @@
 #   c4n1      tools/c4_n1_probe.py: the one-rank rt_render_multi frame against plain c3 renders
 #   hostw     tools/_mb_hostwrite (kernel stores into pinned host memory by store shape)
 #   refill    tools/_var/mb_refill: traced wave durations replayed as sleeps, by LDS / VGPR footprint
+#   abenv     tools/ab_env.py: context settings from the environment, one context each (ABENV_MODES)
+#   sdma      tools/_var/mb_sdma: a frame's device-to-host copy on the SDMA engines vs the runtime's, beside a busy kernel
 #   ab        tools/ab_libs.py over tools/_var/* (VARS=comma list, CONFIGS, ROUNDS; INFLIGHT for the bench pattern)
 #   prof      one-stream rocprofv3 kernel-trace summaries at c2 / c3 / c5 (CONFIGS)
 #   pmc       PMC passes per config (tools/pmc.sh)
@@ -46,11 +48,25 @@ if want hostw; then
 fi
 if want refill; then
   for c in ${REFILL_CONFIGS:-c5 c2}; do
-    gx=960; [ "$c" = "c2" ] && gx=240
+    gx=960; case "$c" in c2*) gx=240;; esac
     timeout -k 10 120 ./tools/_var/mb_refill $c $gx >> "$OUT/refill.jsonl" 2> "$OUT/refill.err" \
         || { echo "refill $c failed"; tail -20 "$OUT/refill.err"; exit 24; }
   done
   cat "$OUT/refill.jsonl"
+fi
+if want abenv; then
+  timeout -k 10 ${AB_TIMEOUT:-600} python -u tools/ab_env.py ${CONFIGS:-c2,c3,c5} ${ROUNDS:-9} ${ABENV_MODES} \
+      > "$OUT/abenv.jsonl" 2> "$OUT/abenv.err" || { echo "abenv failed"; tail -20 "$OUT/abenv.err"; exit 25; }
+  cat "$OUT/abenv.jsonl"
+fi
+if want compsim; then
+  timeout -k 10 180 python -u tools/compaction_sim.py ${COMPSIM_CONFIGS:-c2,c3,c5} > "$OUT/compaction_sim.jsonl" \
+      2> "$OUT/compaction_sim.err" || { echo "compaction_sim failed"; tail -20 "$OUT/compaction_sim.err"; exit 26; }
+  cat "$OUT/compaction_sim.jsonl"
+fi
+if want sdma; then
+  timeout -k 10 120 ./tools/_var/mb_sdma > "$OUT/sdma.jsonl" 2> "$OUT/sdma.err" || { echo "sdma probe failed"; tail -20 "$OUT/sdma.err"; exit 27; }
+  cat "$OUT/sdma.jsonl"
 fi
 if want ab; then
   VARS=${VARS:-} timeout -k 10 ${AB_TIMEOUT:-600} python -u tools/ab_libs.py ${CONFIGS:-c2,c3,c5} ${ROUNDS:-9} \
