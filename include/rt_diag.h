@@ -43,11 +43,19 @@ int rt_diag_tile_order(rt_ctx* ctx, int mode);
 /* Registers per work-item (*vgprs) and private scratch bytes per work-item (*scratch_bytes) of the render
  * kernel instance rt_render_dev launches for `depth` (0..7) and scene kind `variant`: 0 spheres + board,
  * 1 >= 16 spheres (wave-culling variant), 2 meshes or transparent materials, 3 ray trees (whose node stack
- * lives in scratch by design).  Needs a HIP device.  RT_EINVAL for bad arguments. */
+ * lives in scratch by design), 4 / 5 the achromatic (one-channel) instances of 0 / 1 (depth <= 3; RT_EINVAL
+ * for deeper ones).  Needs a HIP device.  RT_EINVAL for bad arguments. */
 int rt_diag_kernel_resources(int depth, int variant, int* vgprs, int* scratch_bytes);
 
 /* Workgroups per CU the HIP runtime allows the render kernel (depth, variant) with lds_bytes of dynamic LDS. */
 int rt_diag_kernel_occupancy(int depth, int variant, int lds_bytes, int* blocks_per_cu);
+
+/* How this context's last rt_render_packed / rt_render_packed_async frame reached host memory: *mode 0 the copy
+ * kernel on the copy stream, 1 behind the render on the render stream (copy kernel, or hipMemcpyAsync for pageable
+ * memory), 2 stored by the render straight into mapped pinned memory, 3 an SDMA engine, -1 no packed frame yet;
+ * *writer how an SDMA frame's start is signalled (1 the stream's write-value operation, 2 a one-wave kernel, 0 the
+ * engine is not set up).  RT_EINVAL for a null context. */
+int rt_diag_copy_path(rt_ctx* ctx, int* mode, int* writer);
 
 #ifdef __cplusplus
 }

@@ -178,9 +178,10 @@ SIGNATURES = {
     "rt_diag_tile_order": (c_int, [c_void_p, c_int]),
     "rt_diag_kernel_resources": (c_int, [c_int, c_int, _P(c_int), _P(c_int)]),
     "rt_diag_kernel_occupancy": (c_int, [c_int, c_int, c_int, _P(c_int)]),
+    "rt_diag_copy_path": (c_int, [c_void_p, _P(c_int), _P(c_int)]),
 }
 
-_DIAG = {"rt_diag_tile_order", "rt_diag_kernel_resources", "rt_diag_kernel_occupancy"}
+_DIAG = {"rt_diag_tile_order", "rt_diag_kernel_resources", "rt_diag_kernel_occupancy", "rt_diag_copy_path"}
 _lib = None
 
 

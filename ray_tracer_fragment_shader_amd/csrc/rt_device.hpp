@@ -1223,15 +1223,21 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
 #ifndef RT_MAT_UNIFORM
 #define RT_MAT_UNIFORM 0
 #endif
-template <bool FULL, bool CULL, bool ACC = false, int SS = 256>
+// ACHRO (an achromatic scene, rt_scene_achromatic: every light colour and every material term an object uses has
+// R = G = B): the three channels are the same operations on equal values, so only R is computed and the colour is
+// (R, R, R) — bit for bit the reference's (G and B are R's operations repeated).  Not with FULL (transparency weights).
+template <bool FULL, bool CULL, bool ACC = false, int SS = 256, bool ACHRO = false>
 __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, int mat, double ks,
                                     int skip = -1, double* acc = nullptr) {
+    static_assert(!(ACHRO && FULL), "achromatic shading is for opaque scenes");
     const DevScene* S = V.S;
     d3 color = mk(0.0, 0.0, 0.0);
     if (ACC) {
         acc[0] = 0.0;
-        acc[SS] = 0.0;
-        acc[2 * SS] = 0.0;
+        if (!ACHRO) {
+            acc[SS] = 0.0;
+            acc[2 * SS] = 0.0;
+        }
     }
     Ray sr;
     sr.p0 = p;
@@ -1247,7 +1253,14 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
         if (CULL && !FULL && V.np >= kConeMin) m = shadow_bundle_mask(V, hit, sr, i);
         bool lit = false;
         if (hit) lit = !(FULL ? occluded_transparent(V, sr) : occluded<false, CULL>(V, sr, i, m, skip));
-        if (lit) {
+        if (lit && ACHRO) {                                 // R only (same operations as below, channel x)
+            const double a = S->att / (S->att + dl * dl);   // attenuation (:1181)
+            const double lc = a * S->light[i].col[0];       // :1223
+            const DevMat& M = S->mat[mat];
+            const double term = (M.amb[0] * lc + kd * (M.diff[0] * lc)) + ks * (M.spec[0] * lc);   // :1224-1226
+            if (ACC) acc[0] = acc[0] + term;
+            else color.x = color.x + term;
+        } else if (lit) {
             double a = S->att / (S->att + dl * dl);         // attenuation (:1181)
             d3 lC = scl(a, ld3(S->light[i].col));           // :1223
 #if RT_MAT_UNIFORM
@@ -1285,7 +1298,7 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
             }
         }
     }
-    return color;
+    return ACHRO ? mk(color.x, color.x, color.x) : color;
 }
 
 // The fast loop (non-CULL, opaque) at depth 1 accumulates each level's colour in its LDS slot (shade ACC), which
@@ -1330,12 +1343,14 @@ __device__ __forceinline__ d3 continuation(const SceneView& V, int kind, int mat
 }
 
 // A hit at level lvl: park its colour (and, TRANSP, its material for the weight w) in LDS.
-template <bool TRANSP, int SS = kSlotStride>
+template <bool TRANSP, int SS = kSlotStride, bool ACHRO = false>
 __device__ __forceinline__ void park_level(int lvl, int mat, d3 c, double* slot, int* mslot) {
     double* sl = slot + 3 * lvl * SS;
     sl[0] = c.x;
-    sl[SS] = c.y;
-    sl[2 * SS] = c.z;
+    if (!ACHRO) {                                           // (achromatic: G = B = R)
+        sl[SS] = c.y;
+        sl[2 * SS] = c.z;
+    }
     if (TRANSP) mslot[lvl * SS] = mat;
 }
 
@@ -1359,7 +1374,7 @@ __device__ __forceinline__ void next_ray(d3 p, d3 nd, d3 nu, Ray* r) {
 
 // One bounce level of the CULL variant, run by all lanes of the wave (ray_bundle_mask and shade's
 // shadow_bundle_mask reduce over it).  Returns false when no lane hit (the bounce loop ends).
-template <int B, bool TRANSP, int SS = kSlotStride>
+template <int B, bool TRANSP, int SS = kSlotStride, bool ACHRO = false>
 __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool first, bool alive, uint64_t cone, Ray* r, int* levels,
                                            double* slot, int* mslot, int* skip, bool lazy_u, d3* last) {
     // the last level's colour stays in registers (RT_CULL_LAST_REG): slot B does not exist, so the continuation
@@ -1408,7 +1423,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
             asm volatile("" ::: "memory");
         }
     }
-    const d3 c = shade<TRANSP, true>(V, hit, p, n, mat, ks, *skip);
+    const d3 c = shade<TRANSP, true, false, 256, ACHRO>(V, hit, p, n, mat, ks, *skip);
     d3 nu = nd;
     if (hit) {
         if (kParkCull && lvl < B) {
@@ -1419,7 +1434,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
             else nu = mk(psl[3 * SS], psl[4 * SS], psl[5 * SS]);
         }
         if (kLastReg && lvl == B) *last = c;
-        else park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
+        else park_level<TRANSP, SS, ACHRO>(lvl, mat, c, slot, mslot);
         *levels = lvl + 1;
     }
     if (lvl < B) {
@@ -1429,7 +1444,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     return true;
 }
 
-template <int B, bool PRIMARY, bool TRANSP, bool CULL, int SS = kSlotStride>
+template <int B, bool PRIMARY, bool TRANSP, bool CULL, int SS = kSlotStride, bool ACHRO = false>
 __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t cone,
                                     uint32_t* seg, uint32_t* shadow, double* slot, int* mslot) {
     const DevScene* S = V.S;
@@ -1460,7 +1475,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t c
         if (!__any(alive)) break;                           // the whole wave has missed: early out
         const bool first = PRIMARY && lvl == 0;
         if (CULL) {
-            if (!cull_level<B, TRANSP, SS>(V, lvl, first, alive, cone, &r, &levels, slot, mslot,
+            if (!cull_level<B, TRANSP, SS, ACHRO>(V, lvl, first, alive, cone, &r, &levels, slot, mslot,
                                            &skip, lazy_u, &last))
                 break;
         } else {
@@ -1512,7 +1527,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t c
                     ndsl[2 * SS] = nd.z;
                     asm volatile("" ::: "memory");          // keep it in LDS across the light loop
                 }
-                const d3 c = shade<TRANSP, false, kAcc, SS>(V, true, p, n, mat, ks, skip, psl);
+                const d3 c = shade<TRANSP, false, kAcc, SS, ACHRO>(V, true, p, n, mat, ks, skip, psl);
                 if ((kPark || RT_PARK_NU) && lvl < B) {
                     asm volatile("" ::: "memory");
                     nd = mk(ndsl[0], ndsl[SS], ndsl[2 * SS]);
@@ -1520,7 +1535,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t c
                     nu = mk(psl[3 * SS], psl[4 * SS], psl[5 * SS]);
 #endif
                 }
-                if (!kAcc) park_level<TRANSP, SS>(lvl, mat, c, slot, mslot);
+                if (!kAcc) park_level<TRANSP, SS, ACHRO>(lvl, mat, c, slot, mslot);
                 levels = lvl + 1;
             }
 #if RT_KEEP_NU || RT_PARK_NU
@@ -1536,6 +1551,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t c
         const double* sl = slot + 3 * lvl * SS;
         d3 c;
         if (kLastReg && lvl == B) c = last;             // (RT_CULL_LAST_REG: level B's colour in registers)
+        else if (ACHRO) c = mk(sl[0], sl[0], sl[0]);
         else c = mk(sl[0], sl[SS], sl[2 * SS]);
         if (lvl == levels - 1) acc = c;
         else acc = TRANSP ? add(c, had(ld3(S->mat[mslot[lvl * SS]].w), acc)) : add(c, acc);

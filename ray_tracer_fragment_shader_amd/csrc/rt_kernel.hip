@@ -6,7 +6,9 @@
 //   rt_trace_rays_kernel<B>   rayTraceRay on an arbitrary ray list (rt_render.hpp)
 //   rt_prepare_kernel         per-eye sphere data, board numerator and cull flag (once per camera eye)
 //   rt_scene_init_kernel      device-side reciprocals of constant divisors (once per scene)
-//   rt_order_kernel           longest-first tile-row order from a calibration render
+//   rt_rowsum_kernel, rt_order_kernel, rt_disp_kernel
+//                             the dispatch table of a calibrated view: tile rows (or tiles, hipCUB radix sort)
+//                             longest first from a calibration render's per-tile wave times
 //   rt_intersect_kernel       g_scene.intersection on an arbitrary ray list (primitive KATs)
 //   rt_unpack_kernel          multi-GPU: gathered row bands -> image order, packed pixels -> RGBA
 //   rt_raysum_kernel          rt_render's ray statistics
@@ -14,6 +16,9 @@
 // Reference: /root/reference/Hw4/MySdlApplication.cpp (rayTraceScreen :1251-1324, rayTraceRay
 // :1184-1249, intersection code :611-823, :1084-1113).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <array>
@@ -72,16 +77,53 @@ __global__ __launch_bounds__(1024) void rt_order_kernel(const uint32_t* __restri
     for (int k = threadIdx.x; k < n; k += blockDim.x) order[k] = (int32_t)(key[k] & 0xffffffffu);
 }
 
-// The calibration render's per-tile primary cone masks (by tile: ty * tiles_x + tx) into dispatch order
-// (position gy * tiles_x + tx, tile row order[gy], stored at cone_slot: grouped by XCD), for the later renders
-// of the same view.
-__global__ __launch_bounds__(256) void rt_cone_permute_kernel(const uint64_t* __restrict__ by_tile,
-                                                              const int32_t* __restrict__ order, int tiles_x,
-                                                              int tiles_y, uint64_t* __restrict__ by_dispatch) {
+// Per tile row, the sum of its tiles' wave times (the row order's cost); one workgroup per row.
+__global__ __launch_bounds__(256) void rt_rowsum_kernel(const uint32_t* __restrict__ tile_cost, int tiles_x,
+                                                        uint32_t* __restrict__ row_cost) {
+    __shared__ uint32_t part[256];
+    uint32_t acc = 0;
+    for (int x = threadIdx.x; x < tiles_x; x += 256) acc += tile_cost[(size_t)blockIdx.x * tiles_x + x];
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) row_cost[blockIdx.x] = part[0];
+}
+
+__global__ __launch_bounds__(256) void rt_iota_kernel(int32_t* __restrict__ v, int n) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k < n) v[k] = k;
+}
+
+// The dispatch table of a calibrated view: position L (linear workgroup id, L = gy * tiles_x + bx) traces tile
+// by_pos[L] (tile order: tile indices by decreasing calibrated time) or, row order (by_pos = nullptr), tile column
+// tile_col(bx, gy) of tile row row_order[gy]; with the calibration render's per-tile primary cone masks when
+// `cone` (else 0).  Stored at cone_slot(L): grouped by the XCD workgroup L runs on.
+__global__ __launch_bounds__(256) void rt_disp_kernel(const int32_t* __restrict__ row_order,
+                                                      const int32_t* __restrict__ by_pos,
+                                                      const uint64_t* __restrict__ cone, int tiles_x, int tiles_y,
+                                                      DispRec* __restrict__ disp) {
     const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x, n = (size_t)tiles_x * tiles_y;
     if (k >= n) return;
-    const int gy = (int)(k / tiles_x), bx = (int)(k - (size_t)gy * tiles_x);
-    by_dispatch[cone_slot(k, n)] = by_tile[(size_t)order[gy] * tiles_x + tile_col(bx, gy, tiles_x)];
+    int tx, ty;
+    if (by_pos) {
+        const int t = by_pos[k];
+        ty = t / tiles_x;
+        tx = t - ty * tiles_x;
+    } else {
+        const int gy = (int)(k / tiles_x), bx = (int)(k - (size_t)gy * tiles_x);
+        ty = row_order[gy];
+        tx = tile_col(bx, gy, tiles_x);
+    }
+    const uint64_t m = cone ? cone[(size_t)ty * tiles_x + tx] : 0;
+    DispRec r;
+    r.cone_lo = (uint32_t)m;
+    r.cone_hi = (uint32_t)(m >> 32);
+    r.tile = ((uint32_t)ty << 16) | (uint32_t)tx;
+    r.pad = 0;
+    disp[cone_slot(k, n)] = r;
 }
 
 // Per-eye primary-ray sphere data (run by rt_render_dev when the camera eye changes): deltaP = C - eye
@@ -390,9 +432,18 @@ struct rt_ctx {
     // HSA_ENABLE_SDMA / GPU_BLIT_ENGINE_TYPE say), and its pipelined rate settles in one of three states per process
     // (59, 95 or 290 us) — so the product uses its own copy kernel for both calls: behind the render on `rs` for
     // rt_render_packed, on `cs` with 16 workgroups (a copy beside the next render takes CUs from it: fewer
-    // workgroups leave it more) after a cross-stream event for rt_render_packed_async.  RT_COPY_MODE (1: rs, 0: cs,
-    // 2: the kernel stores straight into the pinned buffer — 290 us: single-byte stores over PCIe), RT_COPY_KERNEL
-    // (0: hipMemcpyAsync) and RT_COPY_BLOCKS override (A/B; -1 / 0: the defaults above).
+    // workgroups leave it more) after a cross-stream event for rt_render_packed_async.
+    // r05: the HSA runtime does reach the SDMA engines (hsa_amd_memory_async_copy_on_engine; tools/mb_sdma.cpp: engines
+    // 0-3 move the frame at 44.5 GB/s, 46 us, and take nothing from a kernel running beside them), and a copy queued
+    // with a dependency signal that the render stream fires starts without the host (copy_mode 3, sd_* below).
+    // tools/copy_ab.py, same box, 60 frames x 5 rounds:   synchronous   pipelined (wait f-1)   (wait f-2)
+    //   copy kernel behind the render (rs)                    79.3          69.9                  70.2
+    //   copy kernel on the copy stream (cs), 16 WGs           95.2          85.3                  85.7
+    //   SDMA engine behind the render                         81.6          49.6                  49.5
+    // So rt_render_packed_async defaults to the SDMA engine for page-locked buffers (the copy stream for others or
+    // when no engine is free) and rt_render_packed to the copy kernel behind the render.  RT_COPY_MODE (1: rs, 0: cs,
+    // 2: the kernel stores straight into the pinned buffer — 290 us: single-byte stores over PCIe, 3: SDMA),
+    // RT_COPY_KERNEL (0: hipMemcpyAsync) and RT_COPY_BLOCKS override (A/B; -1 / 0: the defaults above).
     int copy_mode = -1;
     int copy_kernel = -1;
     int copy_blocks = 0;                       // RT_COPY_BLOCKS: workgroups of the copy kernel (0: the defaults above)
@@ -404,9 +455,21 @@ struct rt_ctx {
     // re-times the rows under it, so a moving camera keeps a longest-first order without paying for a
     // calibration every frame.  Any order is a permutation of the tile rows: images never depend on it.
     // order_mode (rt_diag_tile_order): 0 adaptive, 1 bottom-to-top.
-    int32_t* d_tile_rows = nullptr;
-    uint32_t* d_row_cost = nullptr;
+    int32_t* d_tile_rows = nullptr;            // row order: tile rows by decreasing calibrated time
+    uint32_t* d_row_cost = nullptr;            // ... their times (rt_rowsum_kernel)
     int n_tile_rows = 0;                       // capacity of both (kOrderMax, allocated by rt_ctx_create)
+    // The view's dispatch table (rt_disp_kernel) and what builds it, per tile (view_cap tiles each): the calibration
+    // render's wave times (d_tile_cost) and cone masks (d_cone_tile), and the tile order's radix-sort buffers.
+    // order_policy (RT_ORDER_POLICY): 0 tile rows longest first (r01-r04), 1 tiles longest first.
+    DispRec* d_disp = nullptr;
+    uint32_t* d_tile_cost = nullptr;
+    uint32_t* d_sort_keys = nullptr;
+    int32_t* d_sort_in = nullptr;
+    int32_t* d_sort_out = nullptr;
+    void* d_sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    size_t view_cap = 0;
+    int order_policy = 0;
     using ViewKey = std::array<unsigned char, sizeof(rt_camera) + 6 * sizeof(int) + sizeof(rt_rows) + sizeof(uint64_t)>;
     bool order_valid = false;                  // d_tile_rows holds the order of view `order_key`
     ViewKey order_key{};
@@ -415,16 +478,14 @@ struct rt_ctx {
     int stale = 0;                             // renders of other cameras since the order was calibrated
     int order_mode = 0;
     // Primary cone masks of the calibrated view (scenes with >= kPrimaryConeMin spheres): the calibration render
-    // writes each tile's mask (d_cone_tile), rt_cone_permute_kernel puts them in dispatch order (d_cone_disp),
-    // and later renders of exactly that view (order_key) read them instead of recomputing them.  Renders of
-    // another camera compute their own.  One-wave (8 x 8 tile) variants only.  Ordering against renders on
-    // other streams: view_ev and the reader tracking below.
+    // writes each tile's mask (d_cone_tile), rt_disp_kernel puts them in the dispatch table, and later renders of
+    // exactly that view (order_key) read them instead of recomputing them.  Renders of another camera compute their
+    // own.  One-wave (8 x 8 tile) variants only.  Ordering against renders on other streams: view_ev and the reader
+    // tracking below.
     uint64_t* d_cone_tile = nullptr;
-    uint64_t* d_cone_disp = nullptr;
-    size_t cone_cap = 0;                       // tiles each holds
-    bool cone_valid = false;                   // d_cone_disp holds the masks of view order_key
+    bool cone_valid = false;                   // d_disp holds the masks of view order_key
     // Cross-stream ordering of the per-view state: the per-eye records inside d_scene (rt_prepare_kernel) and the
-    // calibration buffers (d_row_cost, d_tile_rows, d_cone_tile, d_cone_disp).  Every render reads the per-eye
+    // calibration buffers (d_row_cost, d_tile_rows, d_tile_cost, d_cone_tile, d_disp).  Every render reads the per-eye
     // records; a render that prepares a new eye or calibrates also writes.  A writer records view_ev on its stream
     // after its last write; a render on another stream first waits for view_ev on the GPU (read-after-write,
     // write-after-write).  Renders are tracked by stream: a writer drains the device first when renders were queued
@@ -437,6 +498,7 @@ struct rt_ctx {
     bool readers = false;                      // ... (any)
     bool readers_multi = false;                // ... on more than one stream
     int cone_cache = RT_CONE_CACHE_DEFAULT;    // RT_CONE_CACHE=0: always compute the masks in the kernel (A/B)
+    bool achro_off = false;                    // RT_ACHRO_OFF=1: the three-channel kernels for achromatic scenes (A/B)
     uint64_t scene_gen = 0;
     uint64_t scene_hash = 0;                   // FNV-1a of `blob` (rt_ctx_scene_id)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -451,6 +513,17 @@ struct rt_ctx {
     hipEvent_t copied[kSlots] = {};            // slot b's packed frame is in its host buffer
     bool copied_rec[kSlots] = {};
     bool copied_cs[kSlots] = {};               // ... by a copy on the copy stream (else on the render stream)
+    // copy_mode 3: the frame leaves on a copy (SDMA) engine — no CUs taken from the next render.  Per slot, the
+    // render stream stores 0 into sd_dep (hipStreamWriteValue64 on the HSA signal's value) once the frame is in its
+    // device buffer; the SDMA copy, queued with sd_dep as its dependency, then moves it and decrements sd_done.
+    bool sd_tried = false, sd_ok = false;
+    hsa_agent_t sd_gpu{0}, sd_cpu{0};
+    uint32_t sd_engine = 0;
+    hsa_signal_t sd_dep[kSlots] = {}, sd_done[kSlots] = {};
+    volatile hsa_signal_value_t* sd_dep_ptr[kSlots] = {};
+    bool sd_pending[kSlots] = {};
+    int sd_writer = 0;                                  // sdma_fire: 1 stream write-value, 2 signal kernel
+    int last_copy_mode = -1;                            // the mode the last packed frame took (rt_diag_copy_path)
     uint64_t ticket = 0;                       // rt_render_packed_async frames queued so far
     // rt_render's device buffers (grow-only, reused across calls): rgba32f, rgba8, rgb64f, raycount, sums,
     // packed slot 0, packed slot 1
@@ -495,6 +568,49 @@ extern "C" int rt_device_count(int* count) {
     return RT_OK;
 }
 
+// The per-tile view buffers (dispatch table, tile times, cone masks, sort buffers) of a context.
+static void rt_free_view_bufs(rt_ctx* c) {
+    void* bufs[] = {c->d_disp, c->d_tile_cost, c->d_cone_tile, c->d_sort_keys, c->d_sort_in, c->d_sort_out,
+                    c->d_sort_tmp};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    c->d_disp = nullptr;
+    c->d_tile_cost = c->d_sort_keys = nullptr;
+    c->d_cone_tile = nullptr;
+    c->d_sort_in = c->d_sort_out = nullptr;
+    c->d_sort_tmp = nullptr;
+    c->sort_tmp_bytes = 0;
+    c->view_cap = 0;
+}
+
+// ... grown to hold `tiles` tiles (the caller has drained the device: renders may read the old ones).  False (and no
+// buffers) when the device is out of memory: the view then keeps the identity order.
+static bool rt_grow_view_bufs(rt_ctx* c, size_t tiles) {
+    if (tiles <= c->view_cap) return true;
+    rt_free_view_bufs(c);
+    const size_t slots = cone_slots(tiles);
+    bool ok = hipMalloc(&c->d_disp, slots * sizeof(DispRec)) == hipSuccess &&
+              hipMalloc(&c->d_tile_cost, tiles * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&c->d_cone_tile, tiles * sizeof(uint64_t)) == hipSuccess &&
+              hipMalloc(&c->d_sort_keys, tiles * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&c->d_sort_in, tiles * sizeof(int32_t)) == hipSuccess &&
+              hipMalloc(&c->d_sort_out, tiles * sizeof(int32_t)) == hipSuccess;
+    if (ok) {
+        size_t tmp = 0;
+        ok = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, c->d_tile_cost, c->d_sort_keys, c->d_sort_in,
+                                                          c->d_sort_out, (int)tiles) == hipSuccess &&
+             hipMalloc(&c->d_sort_tmp, tmp) == hipSuccess;
+        c->sort_tmp_bytes = tmp;
+    }
+    if (!ok) {
+        (void)hipGetLastError();
+        rt_free_view_bufs(c);
+        return false;
+    }
+    c->view_cap = tiles;
+    return true;
+}
+
 extern "C" int rt_ctx_destroy(rt_ctx* c) {
     if (!c) return RT_OK;
     (void)hipSetDevice(c->device);
@@ -504,8 +620,16 @@ extern "C" int rt_ctx_destroy(rt_ctx* c) {
     if (c->d_scene) (void)hipFree(c->d_scene);
     if (c->d_tile_rows) (void)hipFree(c->d_tile_rows);
     if (c->d_row_cost) (void)hipFree(c->d_row_cost);
-    if (c->d_cone_tile) (void)hipFree(c->d_cone_tile);
-    if (c->d_cone_disp) (void)hipFree(c->d_cone_disp);
+    rt_free_view_bufs(c);
+    if (c->sd_ok) {
+        for (int b = 0; b < rt_ctx::kSlots; ++b) {
+            if (c->sd_pending[b]) hsa_signal_wait_scacquire(c->sd_done[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                                            HSA_WAIT_STATE_BLOCKED);
+            hsa_signal_destroy(c->sd_dep[b]);
+            hsa_signal_destroy(c->sd_done[b]);
+        }
+        hsa_shut_down();
+    }
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->view_ev) (void)hipEventDestroy(c->view_ev);
@@ -535,10 +659,12 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_MIN_WAVES")) c->min_waves = atoi(e);
     if (const char* e = getenv("RT_WG_STAGING")) c->wg_staging = atoi(e) != 0;
     if (const char* e = getenv("RT_TILE_ORDER")) c->order_mode = atoi(e) == 1 ? 1 : 0;   // 1: bottom-to-top (A/B)
-    if (const char* e = getenv("RT_COPY_MODE")) c->copy_mode = std::min(std::max(atoi(e), -1), 2);
+    if (const char* e = getenv("RT_COPY_MODE")) c->copy_mode = std::min(std::max(atoi(e), -1), 3);
     if (const char* e = getenv("RT_COPY_BLOCKS")) c->copy_blocks = std::max(atoi(e), 0);
     if (const char* e = getenv("RT_COPY_KERNEL")) c->copy_kernel = std::min(std::max(atoi(e), -1), 1);
     if (const char* e = getenv("RT_CONE_CACHE")) c->cone_cache = atoi(e) != 0;
+    if (const char* e = getenv("RT_ORDER_POLICY")) c->order_policy = std::min(std::max(atoi(e), 0), 1);
+    if (const char* e = getenv("RT_ACHRO_OFF")) c->achro_off = atoi(e) != 0;
     if (hipMalloc(&c->d_tile_rows, sizeof(int32_t) * kOrderMax) != hipSuccess ||
         hipMalloc(&c->d_row_cost, sizeof(uint32_t) * kOrderMax) != hipSuccess) {
         rt_ctx_destroy(c);
@@ -713,7 +839,8 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
     if (capturing) c->ever_captured = true;
     bool calibrate = false, cone_calib = false;
     rt_ctx::ViewKey key{};
-    if (!capturing && c->order_mode == 0 && tiles_y <= c->n_tile_rows) {
+    // (dispatch records pack the tile as ty << 16 | tx)
+    if (!capturing && c->order_mode == 0 && tiles_y <= c->n_tile_rows && tiles_x < 65536 && tiles_y < 65536) {
         // Key of the frame's work: camera, size, outputs, row plan, depth and scene generation.
         unsigned char* kp = key.data();                 // fixed size: no host allocation per render
         memcpy(kp, cam, sizeof(rt_camera)); kp += sizeof(rt_camera);
@@ -730,20 +857,18 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
         const bool same_shape = c->order_valid &&
                                 memcmp(key.data() + kCam, c->order_key.data() + kCam, key.size() - kCam) == 0;
         if (c->order_valid && key == c->order_key) {
-            P.tile_rows = c->d_tile_rows;
+            P.disp = c->d_disp;
             // (the cached masks hold one mask per one-wave 8 x 8 tile: the 256-thread A/B variants never read them)
-            if (c->cone_valid && !big) P.cone_in = c->d_cone_disp;
+            P.cone_use = c->cone_valid && !big ? 1 : 0;
         } else if (same_shape) {
-            P.tile_rows = c->d_tile_rows;               // another camera: the last calibrated order
+            P.disp = c->d_disp;                         // another camera: the last calibrated order, its own masks
             if (++c->stale >= kRecalibrate) {           // ... re-timed every kRecalibrate-th render
-                P.row_cost = c->d_row_cost;
                 calibrate = true;
                 c->order_valid = false;
             }
         } else if (c->seen_valid && key == c->seen_key) {
-            P.row_cost = c->d_row_cost;                 // calibration render (identity order)
-            calibrate = true;
-            c->order_valid = false;                     // rt_order_kernel rewrites d_tile_rows below
+            calibrate = true;                           // calibration render (identity order)
+            c->order_valid = false;                     // rt_disp_kernel rewrites d_disp below
             // the calibration records one mask per tile from lane 0 of its wave: one-wave workgroups only
             cone_calib = c->cone_cache && c->n_padded >= kPrimaryConeMin && !c->tree && !c->transparent && !big &&
                          RT_WG_FAST == 64;
@@ -753,13 +878,13 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
         }
     }
     const bool prepare = capturing || c->ever_captured || !c->eye_valid || memcmp(c->eye, cam->eye, sizeof(c->eye)) != 0;
-    const size_t cone_need = cone_calib ? cone_slots((size_t)tiles_x * tiles_y) : 0;
+    const size_t tiles = (size_t)tiles_x * tiles_y;
     if (!capturing) {                                   // (a captured render carries its own prepare launch)
         // read-after-write / write-after-write: the last write of the view state was queued on another stream
         if (c->view_rec && c->view_st != st) RT_HIP(hipStreamWaitEvent(st, c->view_ev, 0));
         if (prepare || calibrate) {
-            // write-after-read: renders queued on other streams may still read what this render rewrites
-            if ((c->readers && (c->readers_multi || c->reader_st != st)) || cone_need > c->cone_cap)
+            // write-after-read: renders queued on other streams may still read what this render rewrites (or frees)
+            if ((c->readers && (c->readers_multi || c->reader_st != st)) || (calibrate && tiles > c->view_cap))
                 RT_HIP(hipDeviceSynchronize());
             c->readers = c->readers_multi = false;      // same-stream renders are ordered before the rewrite
         }
@@ -771,29 +896,17 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
         }
     }
     if (calibrate) {
+        // the calibration render writes every tile's wave time (and, a static view's, its cone mask); the buffers
+        // grow here (the device was drained above)
         c->cone_valid = false;
-        RT_HIP(hipMemsetAsync(c->d_row_cost, 0, sizeof(uint32_t) * tiles_y, st));
-    }
-    if (cone_calib) {
-        // this (static) view's calibration also records its cone masks (the device is drained above when the
-        // buffers must grow)
-        const size_t need = cone_slots((size_t)tiles_x * tiles_y);
-        if (need > c->cone_cap) {
-            if (c->d_cone_tile) (void)hipFree(c->d_cone_tile);
-            if (c->d_cone_disp) (void)hipFree(c->d_cone_disp);
-            c->d_cone_tile = c->d_cone_disp = nullptr;
-            c->cone_cap = 0;
-            if (hipMalloc(&c->d_cone_tile, need * sizeof(uint64_t)) != hipSuccess ||
-                hipMalloc(&c->d_cone_disp, need * sizeof(uint64_t)) != hipSuccess) {
-                if (c->d_cone_tile) (void)hipFree(c->d_cone_tile);
-                c->d_cone_tile = nullptr;
-                cone_calib = false;                     // no cache: later renders compute their masks
-                (void)hipGetLastError();
-            } else {
-                c->cone_cap = need;
-            }
+        if (!rt_grow_view_bufs(c, tiles)) {             // out of memory: identity order, masks in the kernel
+            calibrate = cone_calib = false;
+            P.disp = nullptr;
+            P.cone_use = 0;
+        } else {
+            P.tile_cost = c->d_tile_cost;
+            if (cone_calib) P.cone_out = c->d_cone_tile;
         }
-        if (cone_calib) P.cone_out = c->d_cone_tile;
     }
     const dim3 grid((unsigned)tiles_x, (unsigned)std::min(tiles_y, kGridY), (unsigned)((tiles_y + kGridY - 1) / kGridY));
     hipError_t e;
@@ -810,6 +923,8 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
         c->eye_valid = true;
     }
     RenderLaunch L;
+    // achromatic opaque scenes: the one-channel instances (rt_device.hpp shade ACHRO; RT_ACHRO_OFF=1 for A/B)
+    L.achro = c->achromatic && !c->transparent && !c->tree && !c->achro_off;
     L.grid = grid;
     L.stream = st;
     L.scene = c->d_scene;
@@ -854,16 +969,26 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
     }
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_kernel launch: ") + hipGetErrorString(e));
     if (calibrate) {
-        hipLaunchKernelGGL(rt_order_kernel, dim3(1), dim3(1024), 0, st, c->d_row_cost, tiles_y, c->d_tile_rows);
-        e = hipGetLastError();
-        if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_order_kernel: ") + hipGetErrorString(e));
-        if (cone_calib) {
-            const size_t n = (size_t)tiles_x * tiles_y;
-            hipLaunchKernelGGL(rt_cone_permute_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                               c->d_cone_tile, c->d_tile_rows, tiles_x, tiles_y, c->d_cone_disp);
-            e = hipGetLastError();
-            if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_cone_permute_kernel: ") + hipGetErrorString(e));
+        // the dispatch table of this view (stream-ordered after the calibration render, which wrote the tile times)
+        const dim3 tg((unsigned)((tiles + 255) / 256));
+        const uint64_t* cones = cone_calib ? c->d_cone_tile : nullptr;
+        if (c->order_policy == 1) {                     // tiles longest first
+            hipLaunchKernelGGL(rt_iota_kernel, tg, dim3(256), 0, st, c->d_sort_in, (int)tiles);
+            size_t tmp = c->sort_tmp_bytes;
+            e = hipcub::DeviceRadixSort::SortPairsDescending(c->d_sort_tmp, tmp, c->d_tile_cost, c->d_sort_keys,
+                                                             c->d_sort_in, c->d_sort_out, (int)tiles, 0, 32, st);
+            if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("tile order sort: ") + hipGetErrorString(e));
+            hipLaunchKernelGGL(rt_disp_kernel, tg, dim3(256), 0, st, nullptr, c->d_sort_out, cones, tiles_x, tiles_y,
+                               c->d_disp);
+        } else {                                        // tile rows longest first
+            hipLaunchKernelGGL(rt_rowsum_kernel, dim3((unsigned)tiles_y), dim3(256), 0, st, c->d_tile_cost, tiles_x,
+                               c->d_row_cost);
+            hipLaunchKernelGGL(rt_order_kernel, dim3(1), dim3(1024), 0, st, c->d_row_cost, tiles_y, c->d_tile_rows);
+            hipLaunchKernelGGL(rt_disp_kernel, tg, dim3(256), 0, st, c->d_tile_rows, nullptr, cones, tiles_x, tiles_y,
+                               c->d_disp);
         }
+        e = hipGetLastError();
+        if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("dispatch table: ") + hipGetErrorString(e));
         c->order_key = key;                             // only once the order kernel is queued
         c->order_valid = true;
         c->cone_valid = cone_calib;
@@ -1006,9 +1131,106 @@ extern "C" int rt_render(rt_ctx* c, const rt_scene* scene, const rt_camera* cam,
     return RT_OK;
 }
 
+// ---- copy_mode 3: device-to-host frames on an SDMA engine (HSA runtime, hsa_amd_memory_async_copy_on_engine) ----
+struct SdmaAgents {
+    uint32_t domain = 0, bdf = 0;
+    hsa_agent_t gpu{0}, cpu{0};
+};
+static hsa_status_t sdma_find_agent(hsa_agent_t a, void* data) {
+    SdmaAgents* f = static_cast<SdmaAgents*>(data);
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+    if (t == HSA_DEVICE_TYPE_CPU && f->cpu.handle == 0) f->cpu = a;
+    if (t == HSA_DEVICE_TYPE_GPU) {
+        uint32_t dom = 0, bdf = 0;
+        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+        if (dom == f->domain && bdf == f->bdf) f->gpu = a;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+__global__ void __launch_bounds__(64) rt_signal_fire_kernel(int64_t* value) {
+    if (threadIdx.x == 0) __hip_atomic_store(value, (int64_t)0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Queue "slot b's frame is in its device buffer" on the render stream: store 0 into sd_dep[b] (writer 1: the
+// stream's write-value operation, 2: a one-wave kernel behind the render).
+static hipError_t sdma_fire(rt_ctx* c, int b, int writer) {
+    if (writer == 1) return hipStreamWriteValue64(c->rs, (void*)c->sd_dep_ptr[b], 0, 0);
+    hipLaunchKernelGGL(rt_signal_fire_kernel, dim3(1), dim3(64), 0, c->rs, (int64_t*)c->sd_dep_ptr[b]);
+    return hipGetLastError();
+}
+
+// The context's GPU agent (matched to its HIP device by PCI domain / bus / device / function), a CPU agent, a free SDMA
+// engine between them and the per-slot signals; false (once, remembered) when any of it is missing.
+static bool sdma_init(rt_ctx* c) {
+    if (c->sd_tried) return c->sd_ok;
+    c->sd_tried = true;
+    char bus[64] = {};
+    unsigned dom = 0, b = 0, d = 0, f = 0;
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, c->device) != hipSuccess ||
+        sscanf(bus, "%x:%x:%x.%x", &dom, &b, &d, &f) != 4 || hsa_init() != HSA_STATUS_SUCCESS)
+        return false;
+    SdmaAgents ag;
+    ag.domain = dom;
+    ag.bdf = (b << 8) | (d << 3) | f;
+    uint32_t mask = 0;
+    if (hsa_iterate_agents(sdma_find_agent, &ag) != HSA_STATUS_SUCCESS || !ag.gpu.handle || !ag.cpu.handle ||
+        hsa_amd_memory_copy_engine_status(ag.cpu, ag.gpu, &mask) != HSA_STATUS_SUCCESS || mask == 0) {
+        hsa_shut_down();
+        return false;
+    }
+    // sd_dep is waited on by the copy engine only (GPU_ONLY: the one kind whose value a stream or kernel may store)
+    bool ok = true;
+    for (int k = 0; k < rt_ctx::kSlots && ok; ++k)
+        ok = hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &c->sd_dep[k]) == HSA_STATUS_SUCCESS &&
+             hsa_signal_create(0, 0, nullptr, &c->sd_done[k]) == HSA_STATUS_SUCCESS &&
+             hsa_amd_signal_value_pointer(c->sd_dep[k], &c->sd_dep_ptr[k]) == HSA_STATUS_SUCCESS;
+    // how the render stream fires it: the stream's own write (hipStreamWriteValue64), else a one-wave kernel's
+    // system-scope store; each is tried once on slot 0's signal and must be seen from the host
+    if (ok) {
+        c->sd_writer = 0;
+        for (int w = 1; w <= 2 && !c->sd_writer; ++w) {
+            hsa_signal_store_screlease(c->sd_dep[0], 1);
+            if (sdma_fire(c, 0, w) == hipSuccess && hipStreamSynchronize(c->rs) == hipSuccess &&
+                hsa_signal_load_scacquire(c->sd_dep[0]) == 0)
+                c->sd_writer = w;
+            (void)hipGetLastError();
+        }
+        ok = c->sd_writer != 0;
+    }
+    if (!ok) {
+        for (int k = 0; k < rt_ctx::kSlots; ++k) {
+            if (c->sd_dep[k].handle) hsa_signal_destroy(c->sd_dep[k]);
+            if (c->sd_done[k].handle) hsa_signal_destroy(c->sd_done[k]);
+        }
+        hsa_shut_down();
+        return false;
+    }
+    c->sd_gpu = ag.gpu;
+    c->sd_cpu = ag.cpu;
+    c->sd_engine = mask & (~mask + 1);                 // the lowest free engine
+    c->sd_ok = true;
+    return true;
+}
+
+// Wait until slot b's SDMA copy is done.  A dependency that never fired (its render failed) is released after 5 s so
+// the engine is not left waiting, and reported.
+static int sdma_wait(rt_ctx* c, int b) {
+    if (!c->sd_pending[b]) return RT_OK;
+    const hsa_signal_value_t v = hsa_signal_wait_scacquire(c->sd_done[b], HSA_SIGNAL_CONDITION_LT, 1,
+                                                           (uint64_t)5e9, HSA_WAIT_STATE_BLOCKED);
+    c->sd_pending[b] = false;
+    if (v < 1) return RT_OK;
+    hsa_signal_store_screlease(c->sd_dep[b], 0);
+    hsa_signal_wait_scacquire(c->sd_done[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+    return rt_fail(RT_EHIP, "rt_render_packed: the frame's SDMA copy did not start within 5 s (render failed?)");
+}
+
 // rt_render_packed / rt_render_packed_async: one image in `format`, copied to host memory.
-// async: the copy kernel goes to the copy stream (pipelined frames: it runs beside the next render), else behind the
-// render on the render stream (see rt_ctx::copy_mode).
+// async: the copy goes to an SDMA engine (or, for pageable memory, the copy kernel on the copy stream; pipelined frames:
+// it runs beside the next render), else behind the render on the render stream (see rt_ctx::copy_mode).
 static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera* cam, int W, int H, int depth,
                                int format, void* host, int slot, bool with_stats, size_t* npx_out, void** sums,
                                bool async) {
@@ -1028,13 +1250,22 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
     void* px = nullptr;
     void* rcb = nullptr;
     // RT_COPY_MODE=2 (A/B): the kernel stores the frame straight into the pinned host buffer (mapped into the
-    // device's address space), no device buffer and no copy
-    const int mode = c->copy_mode >= 0 ? c->copy_mode : (async ? 0 : 1);
+    // device's address space), no device buffer and no copy; 3: an SDMA engine copies it (rt_ctx sd_*)
+    int mode = c->copy_mode >= 0 ? c->copy_mode : (async ? 3 : 1);
+    // (the engine needs page-locked host memory: pageable buffers take the copy-kernel / hipMemcpyAsync path)
+    if (mode == 3 && (!host_device_ptr(host, npx * pb) || !sdma_init(c))) mode = async ? 0 : 1;
+    // the slot's device buffer: an SDMA copy of an earlier frame may still read it (whatever this call's mode)
+    if ((rc = sdma_wait(c, slot))) return rc;
+    c->last_copy_mode = mode;
     void* direct = mode == 2 ? pinned_device_ptr(host, npx * pb) : nullptr;
     if (direct) px = direct;
     else if ((rc = ctx_buffer(c, 5 + slot, npx * pb, &px))) return rc;
     if (with_stats && ((rc = ctx_buffer(c, 3, npx * 4, &rcb)) || (rc = ctx_buffer(c, 4, 16, sums)))) return rc;
     const hipStream_t cs = mode != 0 ? c->rs : c->cs;
+    if (mode == 3) {                                    // before the render is queued: it fires sd_dep
+        hsa_signal_store_relaxed(c->sd_dep[slot], 1);
+        hsa_signal_store_relaxed(c->sd_done[slot], 1);
+    }
     // the slot's device buffer is free once its previous frame's copy has left (ordered by the stream when that
     // copy ran on the render stream)
     if (c->copied_rec[slot] && c->copied_cs[slot]) RT_HIP(hipStreamWaitEvent(c->rs, c->copied[slot], 0));
@@ -1045,6 +1276,19 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
     if (rc) return rc;
     if (with_stats) RT_HIP(hipEventRecord(c->ev1, c->rs));
     if (with_stats && (rc = queue_raysum(c, npx, (uint32_t*)rcb, (unsigned long long*)*sums))) return rc;
+    if (mode == 3) {
+        RT_HIP(sdma_fire(c, slot, c->sd_writer));      // the frame is in px
+        const hsa_status_t hs = hsa_amd_memory_async_copy_on_engine(
+            host, c->sd_cpu, px, c->sd_gpu, npx * pb, 1, &c->sd_dep[slot], c->sd_done[slot],
+            (hsa_amd_sdma_engine_id_t)c->sd_engine, true);
+        if (hs != HSA_STATUS_SUCCESS) {
+            RT_HIP(hipStreamSynchronize(c->rs));
+            return rt_fail(RT_EHIP, "rt_render_packed: hsa_amd_memory_async_copy_on_engine failed");
+        }
+        c->sd_pending[slot] = true;
+        c->copied_rec[slot] = false;
+        return RT_OK;
+    }
     if (cs != c->rs) {
         // the copy runs on the copy stream, so it overlaps the next frame's render
         RT_HIP(hipEventRecord(c->rendered[slot], c->rs));
@@ -1067,7 +1311,11 @@ extern "C" int rt_render_packed(rt_ctx* c, const rt_scene* scene, const rt_camer
                                  &npx, &sums, false);
     if (rc) return rc;
     c->ticket = t;
-    RT_HIP(hipEventSynchronize(c->copied[t % rt_ctx::kSlots]));
+    if (c->sd_pending[t % rt_ctx::kSlots]) {
+        if ((rc = sdma_wait(c, (int)(t % rt_ctx::kSlots)))) return rc;
+    } else {
+        RT_HIP(hipEventSynchronize(c->copied[t % rt_ctx::kSlots]));
+    }
     if (stats) {
         RT_HIP(hipStreamSynchronize(c->rs));
         return read_stats(c, npx, (const unsigned long long*)sums, stats);
@@ -1096,11 +1344,23 @@ extern "C" int rt_ctx_wait(rt_ctx* c, uint64_t ticket) {
     if (ticket == 0) {                                  // everything queued on the context's streams
         RT_HIP(hipStreamSynchronize(c->rs));
         RT_HIP(hipStreamSynchronize(c->cs));
+        for (int b = 0; b < rt_ctx::kSlots; ++b) {
+            const int rc = sdma_wait(c, b);
+            if (rc) return rc;
+        }
         return RT_OK;
     }
     // slot (ticket % kSlots) holds this frame's copy or a later one's (which the GPU orders after it)
     const int sl = (int)(ticket % rt_ctx::kSlots);
+    if (c->sd_pending[sl]) return sdma_wait(c, sl);
     if (c->copied_rec[sl]) RT_HIP(hipEventSynchronize(c->copied[sl]));
+    return RT_OK;
+}
+
+extern "C" int rt_diag_copy_path(rt_ctx* c, int* mode, int* writer) {
+    if (!c) return rt_fail(RT_EINVAL, "rt_diag_copy_path: null context");
+    if (mode) *mode = c->last_copy_mode;
+    if (writer) *writer = c->sd_ok ? c->sd_writer : 0;
     return RT_OK;
 }
 
@@ -1277,7 +1537,7 @@ extern "C" int rt_diag_tile_order(rt_ctx* c, int mode) {
 // launches for `depth` and scene kind `variant` (0 spheres + board, 1 >= kConeMin spheres (CULL),
 // 2 meshes / transparency, 3 ray trees) — the tests assert the default instances never spill.
 extern "C" int rt_diag_kernel_resources(int depth, int variant, int* vgprs, int* scratch_bytes) {
-    if (depth < 0 || depth > RT_MAX_B || variant < 0 || variant > 3 || !vgprs || !scratch_bytes)
+    if (depth < 0 || depth > RT_MAX_B || variant < 0 || variant > 5 || !vgprs || !scratch_bytes)
         return rt_fail(RT_EINVAL, "rt_diag_kernel_resources: bad arguments");
     const void* f = nullptr;
     switch (depth) {
@@ -1301,7 +1561,7 @@ extern "C" int rt_diag_kernel_resources(int depth, int variant, int* vgprs, int*
 // Workgroups of the render kernel (depth, variant as above) the runtime places per CU with `lds_bytes` of
 // dynamic LDS (hipOccupancyMaxActiveBlocksPerMultiprocessor).
 extern "C" int rt_diag_kernel_occupancy(int depth, int variant, int lds_bytes, int* blocks_per_cu) {
-    if (depth < 0 || depth > RT_MAX_B || variant < 0 || variant > 3 || lds_bytes < 0 || !blocks_per_cu)
+    if (depth < 0 || depth > RT_MAX_B || variant < 0 || variant > 5 || lds_bytes < 0 || !blocks_per_cu)
         return rt_fail(RT_EINVAL, "rt_diag_kernel_occupancy: bad arguments");
     const void* f = nullptr;
     switch (depth) {

@@ -114,11 +114,20 @@ __host__ __device__ __forceinline__ int tile_col(int bx, int gy, int tiles_x) {
 #endif
 }
 
-// Slot of dispatch position L (linear workgroup id) in the cached cone-mask buffer of n positions: grouped by
-// L mod 8, the XCD the round-robin dispatcher sends workgroup L to (up to a per-launch rotation), so each XCD
-// reads a contiguous run of the buffer and no L2 line is fetched by more than one XCD.
+// Slot of dispatch position L (linear workgroup id) in the dispatch table of n positions: grouped by L mod 8, the XCD
+// the round-robin dispatcher sends workgroup L to (up to a per-launch rotation), so each XCD reads a contiguous run
+// of the table and no L2 line is fetched by more than one XCD.
 __host__ __device__ __forceinline__ size_t cone_slot(size_t L, size_t n) { return (L & 7) * ((n + 7) >> 3) + (L >> 3); }
 __host__ __device__ __forceinline__ size_t cone_slots(size_t n) { return ((n + 7) >> 3) << 3; }
+
+// One dispatch position of a calibrated view (rt_kernel.hip rt_disp_kernel): the tile its workgroup traces
+// (ty << 16 | tx) and that tile's primary cone mask (valid when RenderParams::cone_use).  The table is indexed by
+// cone_slot(position): one 16-byte scalar load per wave brings both.
+struct alignas(16) DispRec {
+    uint32_t cone_lo, cone_hi;
+    uint32_t tile;
+    uint32_t pad;
+};
 
 struct RenderParams {
     double eye[3];
@@ -140,12 +149,12 @@ struct RenderParams {
     int32_t fmt_8;                             // kFmt8_*: byte image format
     float look32[3], right32[3], upp32[3], eye32[3], pitch32;   // FP32 camera for primary_cone_mask
     float cone_slack;                          // its error bound (render_params)
-    const int32_t* tile_rows;                  // dispatch order of tile rows (nullptr: bottom to top)
-    uint32_t* row_cost;                        // calibration render: per tile row, sum of wave times (100 MHz)
+    const DispRec* disp;                       // dispatch table (nullptr: identity order; the kernel reads its argument)
+    uint32_t* tile_cost;                       // calibration render: each tile's wave time (100 MHz), by tile
     int32_t tile_rows_n;                       // tile rows of this launch
     int32_t tiles_x;                           // tiles per tile row (= grid.x)
     uint64_t* wtrace;                          // RT_WAVE_TRACE builds: per-wave {start, end, HW_ID}
-    const uint64_t* cone_in;                   // this view's primary cone masks in dispatch order (or nullptr)
+    int32_t cone_use;                          // 1: disp's cone masks are this view's (cached primary cone masks)
     uint64_t* cone_out;                        // calibration render: each tile's mask, by tile (or nullptr)
     int32_t ns;                                // stride of the scene's per-sphere arrays (DevScene::n_stride)
 };
@@ -160,8 +169,7 @@ struct RenderArgs {
     void* o8;                                  // byte image (RGBA8 / RGB8 / GRAY8) or nullptr
     double* o64;                               // RGB64F parity image or nullptr
     uint32_t* orc;                             // per-pixel ray counters or nullptr
-    const int32_t* tile_rows;                  // dispatch order of tile rows (nullptr: bottom to top)
-    const uint64_t* cone_in;                   // cached primary cone masks (nullptr: computed in the kernel)
+    const DispRec* disp;                       // dispatch table (nullptr: identity order)
 };
 
 // The output pointers, read from the kernel-argument segment where the stores need them: scalar loads behind an
@@ -250,16 +258,15 @@ __device__ __forceinline__ void store_pixel(const RenderParams& P, size_t k, d3 
 }
 
 template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false,
-          bool PACKED = false, bool FIX64 = false>
+          bool PACKED = false, bool FIX64 = false, bool ACHRO = false>
 __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene, RenderParams P,
-                                            const int32_t* __restrict__ tile_rows,
-                                            const uint64_t* __restrict__ cone_in) {
+                                            const DispRec* __restrict__ disp) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
 #if RT_WAVE_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    const uint64_t t_cal = __builtin_amdgcn_s_memrealtime();   // used by calibration renders (P.row_cost)
+    const uint64_t t_cal = __builtin_amdgcn_s_memrealtime();   // used by calibration renders (P.tile_cost)
     // LDS: [header | DevSphere[np] | DevSpherePrim[np]] (LDS = 1), the per-level colour slots of trace()
     // (slot_bytes), then the output staging tile (12 KB, RT_WG_STAGING only).
     // The scene record is broadcast into LDS once per workgroup; the FP32 filter images stay in global
@@ -295,21 +302,20 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     const int cy = lane >> 3;                      // row inside the tile
     const int bxd = blockIdx.x;                     // 2-D grid: tiles_x x tiles_y
     const int gy = (int)(blockIdx.z * kGridY + blockIdx.y);    // tile rows beyond kGridY go to grid.z
-    const int tx = tile_col(bxd, gy, P.tiles_x);    // the image tile column
-    // (a const __restrict__ kernel argument: a scalar load, issued beside the other argument loads; through
-    // RenderParams it was a vector load the whole prologue waited for)
-    // Padding tiles of the last grid.z slice trace a clamped tile and store nothing (no early return: a branch
-    // here kept the compiler from issuing the scene loads until the tile row had arrived).
-    const int ty_raw = tile_rows ? tile_rows[gy] : gy;
-    // The cached primary cone mask of this dispatch position (cone_in: see below), requested together with the
-    // tile row and waited for with it (the empty asm needs both), so the cache costs no round trip of its own;
-    // without a cache the load reads the scene header instead (a valid address) and the value is unused.
-    // (positions past the last tile row — grid.z padding — read the last row's entry: in bounds, unused)
-    const int gyc = gy < P.tile_rows_n ? gy : P.tile_rows_n - 1;
-    const uint64_t* cone_p = cone_in ? cone_in + cone_slot((size_t)gyc * P.tiles_x + bxd, (size_t)P.tile_rows_n * P.tiles_x)
-                                     : reinterpret_cast<const uint64_t*>(gscene);
-    const uint64_t cone_cached = *cone_p;
-    asm volatile("" ::"s"(cone_cached), "s"(ty_raw));
+    // The tile of this dispatch position and (cached views) its primary cone mask: one 16-byte record of the
+    // dispatch table (a const __restrict__ kernel argument: a scalar load issued beside the other argument loads),
+    // or the identity order.  Padding positions of the last grid.z slice trace a clamped tile and store nothing (no
+    // early return: a branch here kept the compiler from issuing the scene loads until the tile had arrived).
+    int tx = tile_col(bxd, gy, P.tiles_x), ty_raw = gy;
+    uint64_t cone_cached = 0;
+    if (disp) {
+        const size_t n = (size_t)P.tile_rows_n * P.tiles_x, Lp = (size_t)gy * P.tiles_x + bxd;
+        const DispRec rec = disp[cone_slot(Lp < n ? Lp : n - 1, n)];   // (padding positions: in bounds, unused)
+        asm volatile("" ::"s"(rec.cone_lo), "s"(rec.cone_hi), "s"(rec.tile));
+        cone_cached = (uint64_t)rec.cone_lo | ((uint64_t)rec.cone_hi << 32);
+        tx = (int)(rec.tile & 0xffffu);
+        ty_raw = Lp < n ? (int)(rec.tile >> 16) : P.tile_rows_n;
+    }
     const bool pad = (unsigned)ty_raw >= (unsigned)P.tile_rows_n;
     const int ty = pad ? P.tile_rows_n - 1 : ty_raw;
     // the stores' tile row: past every local row for padding positions (their bounds check fails), so no flag
@@ -327,10 +333,9 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     // Per-wave sphere culling (all lanes active here).  The block's rows must be contiguous image rows.
     uint64_t cone = ~0ull;
     RT_COUNT(V.S, kCntWaves, 1);
-    if (P.np >= kPrimaryConeMin && cone_in) {
-        // the mask this view's calibration render computed for this tile, permuted into dispatch order
-        // (rt_cone_permute_kernel): one 8-byte scalar load (a const __restrict__ kernel argument, like
-        // tile_rows) instead of the cone phase
+    if (P.np >= kPrimaryConeMin && P.cone_use) {
+        // the mask this view's calibration render computed for this tile, in its dispatch record (rt_disp_kernel):
+        // no cone phase
         cone = cone_cached;
     } else if (P.np >= kPrimaryConeMin) {
         // Within one frame global_row_of is increasing, so jb - ja == 7 means 8 consecutive rows.
@@ -365,7 +370,7 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     if constexpr (TREE)
         col = trace_tree<B>(V, eye, sp, &seg, &sh);
     else
-        col = trace<B, true, TRANSP, CULL, WG>(V, eye, sp, cone, &seg, &sh, slot, mslot);
+        col = trace<B, true, TRANSP, CULL, WG, ACHRO>(V, eye, sp, cone, &seg, &sh, slot, mslot);
 #if RT_WAVE_TRACE >= 2
     asm volatile("" ::"v"(col.x), "v"(col.y), "v"(col.z));
     const uint64_t t_trace = __builtin_amdgcn_s_memrealtime();   // trace() done, the stores next
@@ -389,8 +394,8 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
             if (O.o64) { O.o64[3 * k] = col.x; O.o64[3 * k + 1] = col.y; O.o64[3 * k + 2] = col.z; }
             if (O.orc) O.orc[k] = seg | (sh << 16);
         }
-        if (P.row_cost && tid == 0 && ty_st < P.tile_rows_n)
-            atomicAdd(P.row_cost + ty_st, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
+        if (P.tile_cost && tid == 0 && ty_st < P.tile_rows_n)
+            P.tile_cost[(size_t)ty_st * P.tiles_x + tx] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal);
 #if RT_WAVE_TRACE
         if (P.wtrace && tid == 0) {
             const size_t w = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
@@ -434,17 +439,18 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
         if (outrc) outrc[k] = strc[tid];
         if (out8) reinterpret_cast<uchar4*>(out8)[k] = st8[tid];
     }
-    if (P.row_cost && tid == 0 && !pad) atomicAdd(P.row_cost + ty, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal));
+    if (P.tile_cost && tid == 0 && !pad)
+        P.tile_cost[(size_t)ty * P.tiles_x + tx] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cal);
 }
 
-// (out32 .. outrc are read by late_outputs() from the argument segment, not through the parameters)
+// (out32 .. outrc are read by late_outputs() from the argument segment, not through the parameters.)
+// The parameter list must match RenderArgs field for field: kernarg_offsets_match below checks it at compile time.
 template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false,
-          bool PACKED = false, bool FIX64 = false>
+          bool PACKED = false, bool FIX64 = false, bool ACHRO = false>
 __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene, RenderParams P,
                                                              void* out32, void* out8, double* out64, uint32_t* outrc,
-                                                             const int32_t* __restrict__ tile_rows,
-                                                             const uint64_t* __restrict__ cone_in) {
-    render_body<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED, FIX64>(gscene, P, tile_rows, cone_in);
+                                                             const DispRec* __restrict__ disp) {
+    render_body<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED, FIX64, ACHRO>(gscene, P, disp);
 }
 
 // The same kernel with its SGPRs capped at RT_FAST_SGPRS (amdgpu_num_sgpr: a constant, hence a kernel of its
@@ -459,12 +465,62 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
 #ifndef RT_FAST_SGPRS
 #define RT_FAST_SGPRS 96
 #endif
-template <int B, int MINW, bool CULL, bool PACKED>
+// (the same parameter list as rt_render_kernel: RenderArgs, checked below)
+template <int B, int MINW, bool CULL, bool PACKED, bool ACHRO = false>
 __global__ __launch_bounds__(RT_WG_FAST, MINW) __attribute__((amdgpu_num_sgpr(RT_FAST_SGPRS)))
 void rt_render_kernel_sg(const DevScene* __restrict__ gscene, RenderParams P, void* out32, void* out8, double* out64,
-                         uint32_t* outrc, const int32_t* __restrict__ tile_rows, const uint64_t* __restrict__ cone_in) {
-    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED>(gscene, P, tile_rows, cone_in);
+                         uint32_t* outrc, const DispRec* __restrict__ disp) {
+    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED, false, ACHRO>(gscene, P, disp);
 }
+
+// r05: the achromatic depth-2 fast kernel (c3) fits 63 VGPRs, so a cap of 78 SGPRs gives it 8 waves per SIMD (58
+// SGPRs spilled to VGPR lanes): c3 -1.2% against the 96-SGPR instance (tools/ab_libs.py, 9 rounds, same frames); the
+// same cap on the depth-1 kernel (c2) ran +2.5%, so only depth RT_SG8_B takes it.
+#ifndef RT_FAST8_SGPRS
+#define RT_FAST8_SGPRS 78
+#endif
+#ifndef RT_SG8_B
+#define RT_SG8_B 2
+#endif
+template <int B, int MINW, bool CULL, bool PACKED, bool ACHRO = true>
+__global__ __launch_bounds__(RT_WG_FAST, MINW) __attribute__((amdgpu_num_sgpr(RT_FAST8_SGPRS)))
+void rt_render_kernel_sg8(const DevScene* __restrict__ gscene, RenderParams P, void* out32, void* out8, double* out64,
+                          uint32_t* outrc, const DispRec* __restrict__ disp) {
+    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED, false, ACHRO>(gscene, P, disp);
+}
+template <int B, bool ACHRO>
+constexpr bool use_sg8() { return ACHRO && B == RT_SG8_B && RT_FAST8_SGPRS > 0; }
+
+// late_outputs() reads the output pointers at offsetof(RenderArgs, ...) of the kernel-argument segment, which lays the
+// kernels' parameters out in order, each at its natural alignment.  The offsets of both kernels' actual parameter
+// lists are computed here from their types and compared with RenderArgs: adding, reordering or re-typing a parameter
+// (or a RenderParams change that moves the pointers) fails to compile instead of storing through a wrong pointer.
+template <typename... A>
+struct KernargLayout {
+    static constexpr size_t offset(size_t i) {
+        constexpr size_t sz[] = {sizeof(A)...}, al[] = {alignof(A)...};
+        size_t off = 0;
+        for (size_t k = 0;; ++k) {
+            off = (off + al[k] - 1) / al[k] * al[k];
+            if (k == i) return off;
+            off += sz[k];
+        }
+    }
+};
+template <typename... A>
+constexpr bool kernarg_offsets_match(void (*)(A...)) {
+    using K = KernargLayout<A...>;
+    return sizeof...(A) == 7 && K::offset(0) == offsetof(RenderArgs, scene) && K::offset(1) == offsetof(RenderArgs, P) &&
+           K::offset(2) == offsetof(RenderArgs, o32) && K::offset(3) == offsetof(RenderArgs, o8) &&
+           K::offset(4) == offsetof(RenderArgs, o64) && K::offset(5) == offsetof(RenderArgs, orc) &&
+           K::offset(6) == offsetof(RenderArgs, disp);
+}
+static_assert(kernarg_offsets_match(&rt_render_kernel<1, 0, 1, false, false>),
+              "rt_render_kernel's parameters must lay out as RenderArgs (late_outputs)");
+static_assert(kernarg_offsets_match(&rt_render_kernel_sg<1, 1, false, false>),
+              "rt_render_kernel_sg's parameters must lay out as RenderArgs (late_outputs)");
+static_assert(kernarg_offsets_match(&rt_render_kernel_sg8<1, 1, false, false>),
+              "rt_render_kernel_sg8's parameters must lay out as RenderArgs (late_outputs)");
 
 // rayTraceRay on a list of rays Line(starts[k], ends[k]).  Rays from arbitrary starts: whether their hit
 // points may skip the bounding-sphere cull is decided per ray (hits_ok_from).
@@ -560,6 +616,7 @@ enum RenderVariant {
 
 struct RenderLaunch {
     int variant;
+    bool achro;                                // achromatic scene: the one-channel instances (opaque variants)
     dim3 grid;
     size_t lds;
     hipStream_t stream;
@@ -594,15 +651,15 @@ RT_DECLARE_DEPTH(4) RT_DECLARE_DEPTH(5) RT_DECLARE_DEPTH(6) RT_DECLARE_DEPTH(7)
 #undef RT_DECLARE_DEPTH
 
 // Body of the per-depth instance files.
-template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG, bool TREE, bool PACKED = false, bool FIX64 = false>
+template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG, bool TREE, bool PACKED = false, bool FIX64 = false,
+          bool ACHRO = false>
 hipError_t launch_render_one(const RenderLaunch& L) {
-    auto kern = rt_render_kernel<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED, FIX64>;
+    auto kern = rt_render_kernel<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED, FIX64, ACHRO>;
     if (L.lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, L.grid, dim3(WG), L.lds, L.stream, L.scene, L.P, L.o32, L.o8, L.o64, L.orc,
-                       L.P.tile_rows, L.P.cone_in);
+    hipLaunchKernelGGL(kern, L.grid, dim3(WG), L.lds, L.stream, L.scene, L.P, L.o32, L.o8, L.o64, L.orc, L.P.disp);
     return hipGetLastError();
 }
 
@@ -611,12 +668,24 @@ hipError_t launch_render_one(const RenderLaunch& L) {
 #ifndef RT_SG_MAX_B
 #define RT_SG_MAX_B 2
 #endif
-template <int B, int MINW, bool PACKED>
+template <int B, int MINW, bool PACKED, bool ACHRO = false>
 hipError_t launch_render_sg(const RenderLaunch& L) {
-    hipLaunchKernelGGL((rt_render_kernel_sg<B, MINW, false, PACKED>), L.grid, dim3(RT_WG_FAST), L.lds, L.stream,
-                       L.scene, L.P, L.o32, L.o8, L.o64, L.orc, L.P.tile_rows, L.P.cone_in);
+    if constexpr (use_sg8<B, ACHRO>())
+        hipLaunchKernelGGL((rt_render_kernel_sg8<B, MINW, false, PACKED, ACHRO>), L.grid, dim3(RT_WG_FAST), L.lds,
+                           L.stream, L.scene, L.P, L.o32, L.o8, L.o64, L.orc, L.P.disp);
+    else
+        hipLaunchKernelGGL((rt_render_kernel_sg<B, MINW, false, PACKED, ACHRO>), L.grid, dim3(RT_WG_FAST), L.lds,
+                           L.stream, L.scene, L.P, L.o32, L.o8, L.o64, L.orc, L.P.disp);
     return hipGetLastError();
 }
+
+// The achromatic (one-channel, rt_device.hpp shade ACHRO) instances: the benchmark depths' fast and culling kernels.
+#ifndef RT_ACHRO
+#define RT_ACHRO 1
+#endif
+#ifndef RT_ACHRO_MAX_B
+#define RT_ACHRO_MAX_B 3
+#endif
 
 template <int B>
 hipError_t launch_render_impl(const RenderLaunch& L) {
@@ -624,6 +693,32 @@ hipError_t launch_render_impl(const RenderLaunch& L) {
         return hipErrorInvalidValue;
     } else {
         constexpr int MW = RT_MINW != 0 ? RT_MINW : kDefaultMinWaves(B);
+        constexpr bool kAchro = RT_ACHRO && B <= RT_ACHRO_MAX_B;
+        if constexpr (kAchro) {
+            if (L.achro) {
+                switch (L.variant) {
+                    case kVarFast:
+                        if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return launch_render_sg<B, MW, false, true>(L);
+                        return launch_render_one<B, 0, MW, false, false, RT_WG_FAST, false, false, false, true>(L);
+                    case kVarCull:
+                        if (RT_CULL_FIX64 && L.P.ns == kCullStride)
+                            return launch_render_one<B, 0, cull_min_waves(B), false, true, RT_WG_FAST, false, false, true,
+                                                     true>(L);
+                        return launch_render_one<B, 0, cull_min_waves(B), false, true, RT_WG_FAST, false, false, false,
+                                                 true>(L);
+                    case kVarFastPacked:
+                        if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return launch_render_sg<B, MW, true, true>(L);
+                        return launch_render_one<B, 0, MW, false, false, RT_WG_FAST, false, true, false, true>(L);
+                    case kVarCullPacked:
+                        if (RT_CULL_FIX64 && L.P.ns == kCullStride)
+                            return launch_render_one<B, 0, cull_min_waves(B), false, true, RT_WG_FAST, false, true, true,
+                                                     true>(L);
+                        return launch_render_one<B, 0, cull_min_waves(B), false, true, RT_WG_FAST, false, true, false,
+                                                 true>(L);
+                    default: break;                     // the other variants: three channels
+                }
+            }
+        }
         switch (L.variant) {
             case kVarFast:
                 if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0) return launch_render_sg<B, MW, false>(L);
@@ -705,6 +800,20 @@ const void* render_kernel_ptr_impl(int variant) {
             case 1: return (const void*)rt_render_kernel<B, 0, kCull, false, true, RT_WG_FAST, false, false, (bool)RT_CULL_FIX64>;
             case 2: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, false>;
             case 3: return (const void*)rt_render_kernel<B, 0, 1, true, false, 64, true>;
+            case 4:                                     // the achromatic (one-channel) instances of 0 and 1
+                if constexpr (RT_ACHRO && B <= RT_ACHRO_MAX_B) {
+                    if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0 && use_sg8<B, true>())
+                        return (const void*)rt_render_kernel_sg8<B, kFast, false, false, true>;
+                    else if constexpr (B <= RT_SG_MAX_B && RT_FAST_SGPRS > 0)
+                        return (const void*)rt_render_kernel_sg<B, kFast, false, false, true>;
+                    else return (const void*)rt_render_kernel<B, 0, kFast, false, false, RT_WG_FAST, false, false, false, true>;
+                }
+                return nullptr;
+            case 5:
+                if constexpr (RT_ACHRO && B <= RT_ACHRO_MAX_B)
+                    return (const void*)rt_render_kernel<B, 0, kCull, false, true, RT_WG_FAST, false, false,
+                                                         (bool)RT_CULL_FIX64, true>;
+                return nullptr;
             default: return nullptr;
         }
     }

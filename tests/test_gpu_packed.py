@@ -256,10 +256,26 @@ def _host_alloc(nbytes):
     return p
 
 
-def test_render_packed_host_sync_and_async(tr):
+# the defaults (synchronous: copy kernel behind the render; pipelined: SDMA engine), the copy kernel for both (on the
+# copy stream), the SDMA engine for both
+COPY_MODES = [None, "0", "3"]
+_SYNC_MODE = {None: 1, "0": 0, "3": 3}    # what rt_diag_copy_path reports after a synchronous pinned frame
+_ASYNC_MODE = {None: 3, "0": 0, "3": 3}   # ... after a pipelined one
+
+
+def _copy_path(t):
+    mode, writer = ctypes.c_int(), ctypes.c_int()
+    abi.check(abi.lib().rt_diag_copy_path(t._ctx, ctypes.byref(mode), ctypes.byref(writer)), "rt_diag_copy_path")
+    return mode.value, writer.value
+
+
+@pytest.mark.parametrize("copy_mode", COPY_MODES, ids=["default", "copy_stream", "sdma"])
+def test_render_packed_host_sync_and_async(tr, monkeypatch, copy_mode):
     """rt_render_packed (synchronous, pinned and pageable host buffers, stats) and rt_render_packed_async (a
     pipelined stream of frames with alternating eyes into two pinned buffers, each waited for by its ticket):
-    every frame equals the device render's bytes."""
+    every frame equals the device render's bytes — with the copy kernel and with the SDMA engine."""
+    if copy_mode:
+        monkeypatch.setenv("RT_COPY_MODE", copy_mode)
     L = abi.lib()
     cfg = scenes.CONFIGS["c2"]
     sa = cfg.scene().to_abi()
@@ -282,6 +298,8 @@ def test_render_packed_host_sync_and_async(tr):
                                          pins[0], None), "rt_render_packed")
             got = np.ctypeslib.as_array(ctypes.cast(pins[0], ctypes.POINTER(ctypes.c_uint8)), (H, W, ch))
             assert np.array_equal(got, want[1][..., :ch]), fmt
+            # a pinned buffer takes the requested engine (the pageable one above cannot)
+            assert _copy_path(t)[0] == _SYNC_MODE[copy_mode], _copy_path(t)
         tickets = []
         for f in range(8):
             tk = ctypes.c_uint64()
@@ -293,6 +311,7 @@ def test_render_packed_host_sync_and_async(tr):
                 got = np.ctypeslib.as_array(ctypes.cast(pins[(f - 1) % 2], ctypes.POINTER(ctypes.c_uint8)), (H, W))
                 assert np.array_equal(got, want[(f - 1) % 2][..., 0]), f - 1
         assert tickets == sorted(tickets) and len(set(tickets)) == 8
+        assert _copy_path(t) == (_ASYNC_MODE[copy_mode], 1 if _ASYNC_MODE[copy_mode] == 3 else _copy_path(t)[1])
         abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
         assert L.rt_ctx_wait(t._ctx, tickets[-1] + 5) == abi.RT_EINVAL
     finally:
@@ -301,10 +320,13 @@ def test_render_packed_host_sync_and_async(tr):
         t.close()
 
 
-def test_render_packed_two_behind_and_mixed_sync(tr):
+@pytest.mark.parametrize("copy_mode", COPY_MODES, ids=["default", "copy_stream", "sdma"])
+def test_render_packed_two_behind_and_mixed_sync(tr, monkeypatch, copy_mode):
     """rt_render_packed_async with two frames waited for behind the one being queued (three pinned buffers, the
-    SDMA copies on the copy stream), interleaved with synchronous rt_render_packed calls (copy kernel on the render
-    stream) that reuse the same device slots: every frame, waited for by its ticket, equals the device render."""
+    copies on the copy stream or the SDMA engine), interleaved with synchronous rt_render_packed calls that reuse the
+    same device slots: every frame, waited for by its ticket, equals the device render."""
+    if copy_mode:
+        monkeypatch.setenv("RT_COPY_MODE", copy_mode)
     L = abi.lib()
     cfg = scenes.CONFIGS["c2"]
     sa = cfg.scene().to_abi()
@@ -333,6 +355,7 @@ def test_render_packed_two_behind_and_mixed_sync(tr):
                 got = np.ctypeslib.as_array(ctypes.cast(pins[(f - 2) % 3], ctypes.POINTER(ctypes.c_uint8)), (H, W))
                 assert np.array_equal(got, want[(f - 2) % 3]), f - 2
         abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
+        assert _copy_path(t)[0] == _SYNC_MODE[copy_mode], _copy_path(t)   # the last frame was synchronous
         for f in (10, 11):
             got = np.ctypeslib.as_array(ctypes.cast(pins[f % 3], ctypes.POINTER(ctypes.c_uint8)), (H, W))
             assert np.array_equal(got, want[f % 3]), f

@@ -781,18 +781,21 @@ def test_render_kernels_do_not_spill(tr):
     L = abi.lib()
     regs, scratch = ctypes.c_int(), ctypes.c_int()
     table = {}
-    for variant in (0, 1, 2, 3):
-        for depth in range(8):
+    for variant in (0, 1, 2, 3, 4, 5):
+        for depth in range(8 if variant < 4 else 4):  # (the achromatic instances 4 / 5: depths 0..3)
             abi.check(L.rt_diag_kernel_resources(depth, variant, ctypes.byref(regs), ctypes.byref(scratch)),
                       "rt_diag_kernel_resources")
             table[(variant, depth)] = (regs.value, scratch.value)
     print(table)
     for depth in range(4):                           # c1..c5: spheres + board, and the culling variant
-        assert table[(0, depth)][1] == 0, (depth, table[(0, depth)])
-        assert table[(1, depth)][1] == 0, (depth, table[(1, depth)])
-        if depth != 2:
-            assert table[(1, depth)][0] <= 72, (depth, table[(1, depth)])   # 7 waves per SIMD
+        for fast, cull in ((0, 1), (4, 5)):          # three-channel and achromatic instances
+            assert table[(fast, depth)][1] == 0, (depth, table[(fast, depth)])
+            assert table[(cull, depth)][1] == 0, (depth, table[(cull, depth)])
+            if depth != 2:
+                assert table[(cull, depth)][0] <= 72, (depth, table[(cull, depth)])   # 7 waves per SIMD
     for depth in range(3):
         assert table[(0, depth)][0] <= 80, (depth, table[(0, depth)])
+        assert table[(4, depth)][0] <= 80, (depth, table[(4, depth)])
+    assert L.rt_diag_kernel_resources(4, 4, ctypes.byref(regs), ctypes.byref(scratch)) == abi.RT_EINVAL
     assert table[(3, 3)][1] > 0                     # the ray-tree node stack lives in scratch by design
     assert L.rt_diag_kernel_resources(8, 0, ctypes.byref(regs), ctypes.byref(scratch)) == abi.RT_EINVAL

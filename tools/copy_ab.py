@@ -3,7 +3,8 @@
 
 Settings (env read at rt_ctx_create): RT_COPY_MODE 1 = copy kernel on the render stream (serial), 0 = copy kernel
 on the context's copy stream (overlaps the next render), 2 = the render kernel stores straight into the pinned
-host buffer (no copy); RT_COPY_BLOCKS = copy-kernel workgroups (0 = auto, up to 1024).  Every setting's frames are
+host buffer (no copy), 3 = an SDMA engine copies it (HSA, no CUs); RT_COPY_BLOCKS = copy-kernel workgroups (0 = auto,
+up to 1024).  Every setting's frames are
 checked byte for byte against a device render; rounds interleave the settings (one process, one GPU)."""
 import ctypes
 import json

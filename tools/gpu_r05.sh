@@ -10,6 +10,7 @@
 #   refill    tools/_var/mb_refill: traced wave durations replayed as sleeps, by LDS / VGPR footprint
 #   abenv     tools/ab_env.py: context settings from the environment, one context each (ABENV_MODES)
 #   sdma      tools/_var/mb_sdma: a frame's device-to-host copy on the SDMA engines vs the runtime's, beside a busy kernel
+#   copyab    tools/copy_ab.py: draw()'s GRAY8 host frame by copy mode (COPY_SETTINGS mode:blocks, 3 = SDMA)
 #   ab        tools/ab_libs.py over tools/_var/* (VARS=comma list, CONFIGS, ROUNDS; INFLIGHT for the bench pattern)
 #   prof      one-stream rocprofv3 kernel-trace summaries at c2 / c3 / c5 (CONFIGS)
 #   pmc       PMC passes per config (tools/pmc.sh)
@@ -67,6 +68,11 @@ fi
 if want sdma; then
   timeout -k 10 120 ./tools/_var/mb_sdma > "$OUT/sdma.jsonl" 2> "$OUT/sdma.err" || { echo "sdma probe failed"; tail -20 "$OUT/sdma.err"; exit 27; }
   cat "$OUT/sdma.jsonl"
+fi
+if want copyab; then
+  SETTINGS=${COPY_SETTINGS:-0:16,3:0,1:0} timeout -k 10 300 python -u tools/copy_ab.py > "$OUT/copy_ab.json" \
+      2> "$OUT/copy_ab.err" || { echo "copy_ab failed"; tail -20 "$OUT/copy_ab.err"; exit 28; }
+  cat "$OUT/copy_ab.json"
 fi
 if want ab; then
   VARS=${VARS:-} timeout -k 10 ${AB_TIMEOUT:-600} python -u tools/ab_libs.py ${CONFIGS:-c2,c3,c5} ${ROUNDS:-9} \

@@ -47,6 +47,10 @@ __global__ void busy(float* out, int iters) {
     if (x == 12345.0f) out[0] = y;
 }
 
+__global__ void fire(int64_t* v) {
+    if (threadIdx.x == 0) __hip_atomic_store(v, (int64_t)0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 static double median(std::vector<double> v) {
     std::sort(v.begin(), v.end());
     return v[v.size() / 2];
@@ -138,17 +142,30 @@ int main() {
                tb.empty() ? -1.0 : median(tb), tb.size(), median(kt), (int)((unsigned char*)h_dst)[777]);
     }
     // GPU-triggered (the draw() design): a kernel writes the frame into d_src on a HIP stream, the stream then stores 0
-    // into an HSA signal (hipStreamWriteValue64 on hsa_amd_signal_value_pointer), and an SDMA copy queued beforehand
-    // with that signal as its dependency moves the frame once it fires.  Checked byte for byte; a dependency that never
-    // fires is released from the host after 100 ms (reported), so no copy is left waiting.
-    if (mask) {
+    // into an HSA signal (GPU_ONLY, so its value pointer may be written) — writer 1: hipStreamWriteValue64, writer 2: a
+    // one-wave kernel's system-scope store — and an SDMA copy queued beforehand with that signal as its dependency moves
+    // the frame once it fires.  Checked byte for byte; a dependency that never fires is released from the host after
+    // 100 ms (reported), so no copy is left waiting.
+    for (int writer = 1; writer <= 2 && mask; ++writer) {
         int k = 0;
         while (!(mask & (1u << k))) ++k;
         const hsa_amd_sdma_engine_id_t eng = (hsa_amd_sdma_engine_id_t)(1u << k);
         hsa_signal_t dep;
-        HK(hsa_signal_create(1, 0, nullptr, &dep));
+        HK(hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &dep));
         volatile hsa_signal_value_t* dep_ptr = nullptr;
         HK(hsa_amd_signal_value_pointer(dep, &dep_ptr));
+        hsa_signal_store_screlease(dep, 1);             // can this writer fire it at all?
+        hipError_t we = writer == 1 ? hipStreamWriteValue64(ks, (void*)dep_ptr, 0, 0) : hipSuccess;
+        if (writer == 2) { hipLaunchKernelGGL(fire, dim3(1), dim3(64), 0, ks, (int64_t*)dep_ptr); we = hipGetLastError(); }
+        const hipError_t se = hipStreamSynchronize(ks);
+        printf("{\"writer\": %d, \"queue\": \"%s\", \"sync\": \"%s\", \"fired\": %d}\n", writer, hipGetErrorString(we),
+               hipGetErrorString(se), (int)(hsa_signal_load_scacquire(dep) == 0));
+        fflush(stdout);
+        if (we != hipSuccess || se != hipSuccess || hsa_signal_load_scacquire(dep) != 0) {
+            (void)hipGetLastError();
+            HK(hsa_signal_destroy(dep));
+            continue;
+        }
         std::vector<double> t;
         int bad = 0, released = 0;
         for (int r = 0; r < reps; ++r) {
@@ -158,7 +175,8 @@ int main() {
             auto a = std::chrono::steady_clock::now();
             HK(hsa_amd_memory_async_copy_on_engine(h_dst, g_cpu, d_src, g_gpu, n, 1, &dep, sig, eng, true));
             CK(hipMemsetAsync(d_src, v, n, ks));                                 // "the render"
-            CK(hipStreamWriteValue64(ks, (void*)dep_ptr, 0, 0));
+            if (writer == 1) CK(hipStreamWriteValue64(ks, (void*)dep_ptr, 0, 0));
+            else hipLaunchKernelGGL(fire, dim3(1), dim3(64), 0, ks, (int64_t*)dep_ptr);
             const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(100);
             while (hsa_signal_load_scacquire(sig) != 0) {
                 if (std::chrono::steady_clock::now() > deadline) {                // never fired: release it
@@ -172,8 +190,9 @@ int main() {
             CK(hipStreamSynchronize(ks));
             for (size_t q = 0; q < n; q += 4099) bad += ((unsigned char*)h_dst)[q] != v;
         }
-        printf("{\"copy\": \"sdma%d_after_stream\", \"us_issue_to_done\": %.1f, \"min_us\": %.1f, \"mismatches\": %d, "
-               "\"released_by_host\": %d}\n", k, median(t), *std::min_element(t.begin(), t.end()), bad, released);
+        printf("{\"copy\": \"sdma%d_after_stream\", \"writer\": %d, \"us_issue_to_done\": %.1f, \"min_us\": %.1f, "
+               "\"mismatches\": %d, \"released_by_host\": %d}\n", k, writer, median(t), *std::min_element(t.begin(), t.end()),
+               bad, released);
         HK(hsa_signal_destroy(dep));
     }
     HK(hsa_signal_destroy(sig));

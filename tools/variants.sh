@@ -15,7 +15,7 @@ for spec in "$@"; do
       -fno-fast-math -Wall -Wno-unused-function --offload-arch=gfx950 -DRT_MAX_B=${RT_MAX_B:-3} $flags -c {}.hip -o "$d/{}.o")
   objs=$(for u in $UNITS; do echo "$d/$u.o"; done)
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$d/librt_amd.so" $objs "$LIB/rt_host.o" "$LIB/rt_screen.o" \
-      "$LIB/rt_group.o" "$LIB/rt_group_plan.o" -L/opt/rocm/lib -lrccl
+      "$LIB/rt_group.o" "$LIB/rt_group_plan.o" -L/opt/rocm/lib -lrccl -lhsa-runtime64
   rm -f $objs
   echo "built $name"
 done
