@@ -243,11 +243,11 @@ def kernel_rooflines(cfg_name, nl, W, H, avg_kern_ms):
              "reference_flops_per_launch": ref_flops})
 
 
-ROCPROF_ONE_STREAM = "profiles/r04/{cfg}_kernel_stats_1stream.csv"
+ROCPROF_ONE_STREAM = "profiles/r05/{cfg}_kernel_stats_1stream.csv"
 
 
 def rocprof_reference(cfg_name, full_frame):
-    """The committed one-stream rocprofv3 --kernel-trace --stats summary of this config (tools/gpu_r04_prof.sh:
+    """The committed one-stream rocprofv3 --kernel-trace --stats summary of this config (tools/gpu_r05.sh STEPS=prof:
     bench.py --frames-in-flight 1 --profile-kernel-only): AverageNs of rt_render_kernel is the launch duration,
     so bytes / AverageNs / peak reproduces `frac` from profiles/ alone."""
     path = os.path.join(ROOT, ROCPROF_ONE_STREAM.format(cfg=cfg_name))
@@ -400,8 +400,8 @@ def packed_host_legs(t, sa, cam, W, H, B, k=30):
             out[key] = round((time.perf_counter() - t0) / k * 1e3, 4)
         out["packed_note"] = ("c2 frame as GRAY8 (2.07 MB: the scene is achromatic, rt_scene_achromatic) into pinned "
                               "memory: synchronous per call (render + copy kernel on the render stream), and pipelined "
-                              "(queue frame f, wait for frame f-1 — one frame of latency — or f-2: the copy kernel of a "
-                              "frame on the copy stream runs beside the next frame's render)")
+                              "(queue frame f, wait for frame f-1 — one frame of latency — or f-2: each frame's copy "
+                              "runs on an SDMA engine, started by the render stream, beside the next frame's render)")
     finally:
         for p in pins:
             L.rt_host_free(p)

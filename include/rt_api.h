@@ -238,11 +238,13 @@ int rt_render_dev_packed(rt_ctx* ctx, const rt_camera* cam, int width, int heigh
 /* Host-buffer frames in one format (draw()'s replacement with fewer PCIe bytes).  rt_render_packed is
  * synchronous (stats nullable, as rt_render): the render and a copy kernel that writes the frame over PCIe
  * into host_pixels, back to back on the context's render stream.  rt_render_packed_async queues the render
- * on the render stream and the device-to-host copy kernel on the context's copy stream, and
- * returns at once with a ticket: the copy of frame t runs beside the render of frame t+1 (three device
- * buffers: up to two frames may be waited for behind the one being queued); rt_ctx_wait(ctx, t) returns
- * when frame t's pixels are in host_pixels (ticket 0: everything queued).  host_pixels must stay valid until
- * then; pinned memory (rt_host_alloc) makes the copy a true DMA. */
+ * on the render stream and the frame's device-to-host copy behind it — on an SDMA engine when host_pixels is
+ * page-locked (rt_host_alloc; the render stream starts the engine's copy, no CU is taken from the next render),
+ * else a copy kernel on the context's copy stream — and returns at once with a ticket: the copy of frame t runs
+ * beside the render of frame t+1 (three device buffers: up to two frames may be waited for behind the one being
+ * queued); rt_ctx_wait(ctx, t) returns when frame t's pixels are in host_pixels (ticket 0: everything queued).
+ * host_pixels must stay valid until then.  RT_COPY_MODE (read at rt_ctx_create) overrides the path for both calls:
+ * 0 copy kernel on the copy stream, 1 behind the render, 3 SDMA engine. */
 int rt_render_packed(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, int width, int height, int depth,
                      int format, void* host_pixels, rt_stats* stats);
 int rt_render_packed_async(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, int width, int height,
