@@ -162,14 +162,24 @@ struct RenderParams {
 // The render kernels' arguments, in order: the kernel-argument segment lays them out as this struct (each at its
 // natural alignment), which late_outputs() relies on.  (The kernels take them as separate parameters: one
 // by-value struct parameter measured +11 VGPRs in the culling kernel.)
+// The dispatch table's geometry, scalar arguments right after the table, so that gfx950's kernarg preload
+// (-mllvm -amdgpu-kernarg-preload-count=4, Makefile KERNARG_PRELOAD) can hand both to the wave in SGPRs and its
+// first memory access is its dispatch record.  Measured (r05, tools/ab_libs.py, 9 rounds): preloading 4 or 6
+// dwords within +-0.8% of none at c2 / c3 / c5 (and the preloaded registers cost 20 more SGPR spills), so off.
+struct DispGeom {
+    int32_t tiles_x;                           // tiles per tile row (= grid.x)
+    int32_t n;                                 // dispatch positions with a record (tile rows x tiles_x)
+};
+
 struct RenderArgs {
+    const DispRec* disp;                       // dispatch table (nullptr: identity order)
+    int32_t tiles_x, n_disp;                   // its DispGeom (scalars: aggregates are not preloaded)
     const DevScene* scene;
     RenderParams P;
     void* o32;                                 // float image (RGBA32F / GRAY32F) or nullptr
     void* o8;                                  // byte image (RGBA8 / RGB8 / GRAY8) or nullptr
     double* o64;                               // RGB64F parity image or nullptr
     uint32_t* orc;                             // per-pixel ray counters or nullptr
-    const DispRec* disp;                       // dispatch table (nullptr: identity order)
 };
 
 // The output pointers, read from the kernel-argument segment where the stores need them: scalar loads behind an
@@ -260,7 +270,7 @@ __device__ __forceinline__ void store_pixel(const RenderParams& P, size_t k, d3 
 template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false,
           bool PACKED = false, bool FIX64 = false, bool ACHRO = false>
 __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene, RenderParams P,
-                                            const DispRec* __restrict__ disp) {
+                                            const DispRec* __restrict__ disp, DispGeom geom) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
 #if RT_WAVE_TRACE
@@ -309,7 +319,7 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     int tx = tile_col(bxd, gy, P.tiles_x), ty_raw = gy;
     uint64_t cone_cached = 0;
     if (disp) {
-        const size_t n = (size_t)P.tile_rows_n * P.tiles_x, Lp = (size_t)gy * P.tiles_x + bxd;
+        const size_t n = (size_t)geom.n, Lp = (size_t)gy * geom.tiles_x + bxd;
         const DispRec rec = disp[cone_slot(Lp < n ? Lp : n - 1, n)];   // (padding positions: in bounds, unused)
         asm volatile("" ::"s"(rec.cone_lo), "s"(rec.cone_hi), "s"(rec.tile));
         cone_cached = (uint64_t)rec.cone_lo | ((uint64_t)rec.cone_hi << 32);
@@ -447,10 +457,10 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
 // The parameter list must match RenderArgs field for field: kernarg_offsets_match below checks it at compile time.
 template <int B, int LDS, int MINW, bool TRANSP, bool CULL, int WG = kThreads, bool TREE = false,
           bool PACKED = false, bool FIX64 = false, bool ACHRO = false>
-__global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __restrict__ gscene, RenderParams P,
-                                                             void* out32, void* out8, double* out64, uint32_t* outrc,
-                                                             const DispRec* __restrict__ disp) {
-    render_body<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED, FIX64, ACHRO>(gscene, P, disp);
+__global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DispRec* __restrict__ disp, int32_t tiles_x, int32_t n_disp,
+                                                             const DevScene* __restrict__ gscene, RenderParams P,
+                                                             void* out32, void* out8, double* out64, uint32_t* outrc) {
+    render_body<B, LDS, MINW, TRANSP, CULL, WG, TREE, PACKED, FIX64, ACHRO>(gscene, P, disp, DispGeom{tiles_x, n_disp});
 }
 
 // The same kernel with its SGPRs capped at RT_FAST_SGPRS (amdgpu_num_sgpr: a constant, hence a kernel of its
@@ -468,9 +478,10 @@ __global__ __launch_bounds__(WG, MINW) void rt_render_kernel(const DevScene* __r
 // (the same parameter list as rt_render_kernel: RenderArgs, checked below)
 template <int B, int MINW, bool CULL, bool PACKED, bool ACHRO = false>
 __global__ __launch_bounds__(RT_WG_FAST, MINW) __attribute__((amdgpu_num_sgpr(RT_FAST_SGPRS)))
-void rt_render_kernel_sg(const DevScene* __restrict__ gscene, RenderParams P, void* out32, void* out8, double* out64,
-                         uint32_t* outrc, const DispRec* __restrict__ disp) {
-    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED, false, ACHRO>(gscene, P, disp);
+void rt_render_kernel_sg(const DispRec* __restrict__ disp, int32_t tiles_x, int32_t n_disp,
+                         const DevScene* __restrict__ gscene, RenderParams P, void* out32, void* out8, double* out64,
+                         uint32_t* outrc) {
+    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED, false, ACHRO>(gscene, P, disp, DispGeom{tiles_x, n_disp});
 }
 
 // r05: the achromatic depth-2 fast kernel (c3) fits 63 VGPRs, so a cap of 78 SGPRs gives it 8 waves per SIMD (58
@@ -484,9 +495,10 @@ void rt_render_kernel_sg(const DevScene* __restrict__ gscene, RenderParams P, vo
 #endif
 template <int B, int MINW, bool CULL, bool PACKED, bool ACHRO = true>
 __global__ __launch_bounds__(RT_WG_FAST, MINW) __attribute__((amdgpu_num_sgpr(RT_FAST8_SGPRS)))
-void rt_render_kernel_sg8(const DevScene* __restrict__ gscene, RenderParams P, void* out32, void* out8, double* out64,
-                          uint32_t* outrc, const DispRec* __restrict__ disp) {
-    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED, false, ACHRO>(gscene, P, disp);
+void rt_render_kernel_sg8(const DispRec* __restrict__ disp, int32_t tiles_x, int32_t n_disp,
+                          const DevScene* __restrict__ gscene, RenderParams P, void* out32, void* out8, double* out64,
+                          uint32_t* outrc) {
+    render_body<B, 0, MINW, false, CULL, RT_WG_FAST, false, PACKED, false, ACHRO>(gscene, P, disp, DispGeom{tiles_x, n_disp});
 }
 template <int B, bool ACHRO>
 constexpr bool use_sg8() { return ACHRO && B == RT_SG8_B && RT_FAST8_SGPRS > 0; }
@@ -510,10 +522,11 @@ struct KernargLayout {
 template <typename... A>
 constexpr bool kernarg_offsets_match(void (*)(A...)) {
     using K = KernargLayout<A...>;
-    return sizeof...(A) == 7 && K::offset(0) == offsetof(RenderArgs, scene) && K::offset(1) == offsetof(RenderArgs, P) &&
-           K::offset(2) == offsetof(RenderArgs, o32) && K::offset(3) == offsetof(RenderArgs, o8) &&
-           K::offset(4) == offsetof(RenderArgs, o64) && K::offset(5) == offsetof(RenderArgs, orc) &&
-           K::offset(6) == offsetof(RenderArgs, disp);
+    return sizeof...(A) == 9 && K::offset(0) == offsetof(RenderArgs, disp) &&
+           K::offset(1) == offsetof(RenderArgs, tiles_x) && K::offset(2) == offsetof(RenderArgs, n_disp) &&
+           K::offset(3) == offsetof(RenderArgs, scene) && K::offset(4) == offsetof(RenderArgs, P) &&
+           K::offset(5) == offsetof(RenderArgs, o32) && K::offset(6) == offsetof(RenderArgs, o8) &&
+           K::offset(7) == offsetof(RenderArgs, o64) && K::offset(8) == offsetof(RenderArgs, orc);
 }
 static_assert(kernarg_offsets_match(&rt_render_kernel<1, 0, 1, false, false>),
               "rt_render_kernel's parameters must lay out as RenderArgs (late_outputs)");
@@ -659,7 +672,7 @@ hipError_t launch_render_one(const RenderLaunch& L) {
         hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, L.grid, dim3(WG), L.lds, L.stream, L.scene, L.P, L.o32, L.o8, L.o64, L.orc, L.P.disp);
+    hipLaunchKernelGGL(kern, L.grid, dim3(WG), L.lds, L.stream, L.P.disp, L.P.tiles_x, L.P.tile_rows_n * L.P.tiles_x, L.scene, L.P, L.o32, L.o8, L.o64, L.orc);
     return hipGetLastError();
 }
 
@@ -672,10 +685,10 @@ template <int B, int MINW, bool PACKED, bool ACHRO = false>
 hipError_t launch_render_sg(const RenderLaunch& L) {
     if constexpr (use_sg8<B, ACHRO>())
         hipLaunchKernelGGL((rt_render_kernel_sg8<B, MINW, false, PACKED, ACHRO>), L.grid, dim3(RT_WG_FAST), L.lds,
-                           L.stream, L.scene, L.P, L.o32, L.o8, L.o64, L.orc, L.P.disp);
+                           L.stream, L.P.disp, L.P.tiles_x, L.P.tile_rows_n * L.P.tiles_x, L.scene, L.P, L.o32, L.o8, L.o64, L.orc);
     else
         hipLaunchKernelGGL((rt_render_kernel_sg<B, MINW, false, PACKED, ACHRO>), L.grid, dim3(RT_WG_FAST), L.lds,
-                           L.stream, L.scene, L.P, L.o32, L.o8, L.o64, L.orc, L.P.disp);
+                           L.stream, L.P.disp, L.P.tiles_x, L.P.tile_rows_n * L.P.tiles_x, L.scene, L.P, L.o32, L.o8, L.o64, L.orc);
     return hipGetLastError();
 }
 
