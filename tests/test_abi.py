@@ -160,6 +160,7 @@ def test_errors_on_bad_host_args():
     assert L.rt_local_rows(10, ctypes.byref(scenes.rows(4, 2, 2)), ctypes.byref(ctypes.c_int())) == abi.RT_EINVAL
     assert L.rt_set_scene(None, None) == abi.RT_EINVAL
     assert L.rt_diag_tile_order(None, 0) == abi.RT_EINVAL
+    assert L.rt_diag_copy_path(None, None, None) == abi.RT_EINVAL
     assert L.rt_render_dev(None, None, 8, 8, 1, None, None, None, None, None, None) == abi.RT_EINVAL
 
 
