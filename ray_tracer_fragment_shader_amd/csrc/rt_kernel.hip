@@ -611,6 +611,8 @@ static bool rt_grow_view_bufs(rt_ctx* c, size_t tiles) {
     return true;
 }
 
+static int sdma_wait(rt_ctx* c, int b);   // below, with the SDMA path
+
 extern "C" int rt_ctx_destroy(rt_ctx* c) {
     if (!c) return RT_OK;
     (void)hipSetDevice(c->device);
@@ -623,8 +625,7 @@ extern "C" int rt_ctx_destroy(rt_ctx* c) {
     rt_free_view_bufs(c);
     if (c->sd_ok) {
         for (int b = 0; b < rt_ctx::kSlots; ++b) {
-            if (c->sd_pending[b]) hsa_signal_wait_scacquire(c->sd_done[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                                                            HSA_WAIT_STATE_BLOCKED);
+            (void)sdma_wait(c, b);                     // (the render stream has drained: its signal has fired)
             hsa_signal_destroy(c->sd_dep[b]);
             hsa_signal_destroy(c->sd_done[b]);
         }

@@ -2,6 +2,7 @@
 # Round-5 GPU session.  STEPS selects parts (default: tests bench); each GPU step has its own time limit and the
 # script stops at the first failure.
 #   tests     pytest -m gpu
+#   smoke     __graft_entry__.smoke()
 #   bench     the default bench line (N = 1)
 #   rehearse  bench.py --gpus 2 --backend gloo (two ranks sharing the GPU; the c4 leg as a COPY group on rank 0)
 #   trace     per-wave timeline of one c2 / c5 launch (tools/_var/trace, RT_WAVE_TRACE=2 build) with the attribution
@@ -25,6 +26,11 @@ if want tests; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} \
       > "$OUT/gpu_tests.log" 2>&1
   rc=$?; tail -5 "$OUT/gpu_tests.log"; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit $rc; }
+fi
+if want smoke; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+      || { echo "smoke failed"; tail -20 "$OUT/smoke.log"; exit 29; }
+  tail -3 "$OUT/smoke.log"
 fi
 if want trace; then
   cp "$LIB" /tmp/librt_amd.base.so
