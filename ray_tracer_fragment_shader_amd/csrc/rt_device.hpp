@@ -127,7 +127,10 @@ namespace rt {
 // Counter slots of RT_COUNTERS builds.
 enum Counter {
     kCntWaves = 0, kCntConeKept, kCntRayMasks, kCntRayKept, kCntShadowMasks, kCntShadowKept, kCntExactRay,
-    kCntExactShadow, kCntBoardShadow, kCntLevels, kCntExactPrimary, kCntFilterRay, kCntFilterShadow, kCntCount
+    kCntExactShadow, kCntBoardShadow, kCntLevels, kCntExactPrimary, kCntFilterRay, kCntFilterShadow,
+    // active lanes (sum over the counted wave events) of the same events, and of the culling levels' live / hit lanes
+    kCntLanesFilterRay, kCntLanesExactRay, kCntLanesFilterShadow, kCntLanesExactShadow, kCntLanesLevelAlive,
+    kCntLanesLevelHit, kCntCount
 };
 
 struct d3 {
@@ -306,6 +309,16 @@ __device__ __forceinline__ d3 unit(d3 a) {
         if (RT_COUNTERS && (S)->counters && __lane_id() == __builtin_ctzll(__ballot(1)))                       \
             atomicAdd((S)->counters + (slot), (unsigned long long)(v));                                        \
     } while (0)
+// ... of the lanes active at this point (lane utilisation = lanes / (64 x events))
+// (the ballot is taken before RT_COUNT narrows the wave to one lane)
+#define RT_COUNT_BALLOT(S, slot, pred)                                                                         \
+    do {                                                                                                       \
+        if (RT_COUNTERS) {                                                                                     \
+            const unsigned long long n_ = __popcll(__ballot(pred));                                            \
+            RT_COUNT(S, slot, n_);                                                                             \
+        }                                                                                                      \
+    } while (0)
+#define RT_COUNT_LANES(S, slot) RT_COUNT_BALLOT(S, slot, 1)
 
 struct SceneView {
     const DevScene* S;
@@ -724,6 +737,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
         for (uint64_t m = mask & sphere_bits(V.np); m; m &= m - 1) {
             const int k = __builtin_ctzll(m);
             RT_COUNT(S, kCntFilterRay, 1);
+            RT_COUNT_LANES(S, kCntLanesFilterRay);
 #if RT_PRIM_PREFETCH
             // the exact test's record with the filter's (one wait for both, as in primary_sphere)
             const DevSphereF sf = V.sphf[k];
@@ -735,6 +749,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
             const DevSphere& sp = V.sph[k];
 #endif
             RT_COUNT(S, kCntExactRay, 1);
+            RT_COUNT_LANES(S, kCntLanesExactRay);
             d3 q;
             if (sphere_hit(sp, r.p0, r.u, eps, &q)) take_closer(r.p0, q, 1 + k, &kind, &best, hp);   // :811-813
         }
@@ -1090,8 +1105,10 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
             t = fmaf(r.uy, f.vy, t);
             t = fmaf(r.uz, f.vz, t);
             RT_COUNT(S, kCntFilterShadow, 1);
+            RT_COUNT_LANES(S, kCntLanesFilterShadow);
             if (fabsf(t) < f.c || k == skip - 1) continue;
             RT_COUNT(S, kCntExactShadow, 1);
+            RT_COUNT_LANES(S, kCntLanesExactShadow);
             d3 q;
             if (sphere_hit(V.sph[k], r.p0, r.u, eps, &q)) return true;
         }
@@ -1393,6 +1410,8 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
                      : closest_hit<TRANSP, true>(V, *r, &p, smask, TRANSP ? -1 : *skip, lvl > 0);
     }
     const bool hit = kind >= 0;
+    RT_COUNT_BALLOT(V.S, kCntLanesLevelAlive, alive);
+    RT_COUNT_BALLOT(V.S, kCntLanesLevelHit, hit);
     *skip = TRANSP ? -1 : origin_skip(V, kind, r->p0, p);      // this hit's rays start at p
     if (!__any(hit)) return false;
     d3 n = mk(0.0, 0.0, 0.0), nd = n;

@@ -14,7 +14,12 @@ import torch  # noqa: E402
 from ray_tracer_fragment_shader_amd import abi, scenes  # noqa: E402
 
 NAMES = ["waves", "cone_kept", "ray_masks", "ray_kept", "shadow_masks", "shadow_kept", "exact_ray", "exact_shadow",
-         "board_shadow", "levels", "exact_primary", "filter_ray", "filter_shadow"]
+         "board_shadow", "levels", "exact_primary", "filter_ray", "filter_shadow",
+         "lanes_filter_ray", "lanes_exact_ray", "lanes_filter_shadow", "lanes_exact_shadow", "lanes_level_alive",
+         "lanes_level_hit"]
+# lane utilisation of an event = its lanes / (64 x its count)
+UTIL = {"filter_ray": "lanes_filter_ray", "exact_ray": "lanes_exact_ray", "filter_shadow": "lanes_filter_shadow",
+        "exact_shadow": "lanes_exact_shadow", "levels": "lanes_level_alive"}
 path = os.environ.get("LIB", os.path.join(ROOT, "tools", "_var", "cnt", "librt_amd.so"))
 L = ctypes.CDLL(path)
 for fn, (res, args) in abi.SIGNATURES.items():
@@ -37,5 +42,8 @@ for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["c2", "c3", "c5"]
     torch.cuda.synchronize()
     v = dict(zip(NAMES, cnt.cpu().tolist()))
     w = max(v["waves"], 1)
-    print(json.dumps({"config": name, **v, **{f"{k}_per_wave": round(v[k] / w, 3) for k in NAMES[1:]}}), flush=True)
+    util = {f"util_{k}": round(v[u] / 64 / max(v[k], 1), 3) for k, u in UTIL.items()}
+    util["util_level_hit"] = round(v["lanes_level_hit"] / 64 / max(v["levels"], 1), 3)
+    print(json.dumps({"config": name, **v, **{f"{k}_per_wave": round(v[k] / w, 3) for k in NAMES[1:]}, **util}),
+          flush=True)
     L.rt_ctx_destroy(ctx)

@@ -3,6 +3,7 @@
 # script stops at the first failure.
 #   tests     pytest -m gpu
 #   smoke     __graft_entry__.smoke()
+#   counters  tools/counters.py with the RT_COUNTERS=1 build tools/_var/cnt (events and lane utilisation per wave)
 #   bench     the default bench line (N = 1)
 #   rehearse  bench.py --gpus 2 --backend gloo (two ranks sharing the GPU; the c4 leg as a COPY group on rank 0)
 #   trace     per-wave timeline of one c2 / c5 launch (tools/_var/trace, RT_WAVE_TRACE=2 build) with the attribution
@@ -31,6 +32,11 @@ if want smoke; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
       || { echo "smoke failed"; tail -20 "$OUT/smoke.log"; exit 29; }
   tail -3 "$OUT/smoke.log"
+fi
+if want counters; then
+  LIB=tools/_var/cnt/librt_amd.so timeout -k 10 300 python -u tools/counters.py ${CNT_CONFIGS:-c2,c3,c5} \
+      > "$OUT/counters.jsonl" 2> "$OUT/counters.err" || { echo "counters failed"; tail -20 "$OUT/counters.err"; exit 30; }
+  cat "$OUT/counters.jsonl"
 fi
 if want trace; then
   cp "$LIB" /tmp/librt_amd.base.so
