@@ -518,7 +518,8 @@ struct rt_ctx {
     // device buffer; the SDMA copy, queued with sd_dep as its dependency, then moves it and decrements sd_done.
     bool sd_tried = false, sd_ok = false;
     hsa_agent_t sd_gpu{0}, sd_cpu{0};
-    uint32_t sd_engine = 0;
+    uint32_t sd_engine = 0, sd_engine2 = 0;            // the two lowest free engines (sd_engine2 = 0: only one)
+    int sd_split = 2;                                   // RT_SDMA_SPLIT: engines a frame's copy is split over (1, 2)
     hsa_signal_t sd_dep[kSlots] = {}, sd_done[kSlots] = {};
     volatile hsa_signal_value_t* sd_dep_ptr[kSlots] = {};
     bool sd_pending[kSlots] = {};
@@ -661,6 +662,7 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_WG_STAGING")) c->wg_staging = atoi(e) != 0;
     if (const char* e = getenv("RT_TILE_ORDER")) c->order_mode = atoi(e) == 1 ? 1 : 0;   // 1: bottom-to-top (A/B)
     if (const char* e = getenv("RT_COPY_MODE")) c->copy_mode = std::min(std::max(atoi(e), -1), 3);
+    if (const char* e = getenv("RT_SDMA_SPLIT")) c->sd_split = std::min(std::max(atoi(e), 1), 2);
     if (const char* e = getenv("RT_COPY_BLOCKS")) c->copy_blocks = std::max(atoi(e), 0);
     if (const char* e = getenv("RT_COPY_KERNEL")) c->copy_kernel = std::min(std::max(atoi(e), -1), 1);
     if (const char* e = getenv("RT_CONE_CACHE")) c->cone_cache = atoi(e) != 0;
@@ -1212,6 +1214,8 @@ static bool sdma_init(rt_ctx* c) {
     c->sd_gpu = ag.gpu;
     c->sd_cpu = ag.cpu;
     c->sd_engine = mask & (~mask + 1);                 // the lowest free engine
+    const uint32_t rest = mask & ~c->sd_engine;
+    c->sd_engine2 = rest & (~rest + 1);                 // and the next (0: none)
     c->sd_ok = true;
     return true;
 }
@@ -1263,9 +1267,15 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
     else if ((rc = ctx_buffer(c, 5 + slot, npx * pb, &px))) return rc;
     if (with_stats && ((rc = ctx_buffer(c, 3, npx * 4, &rcb)) || (rc = ctx_buffer(c, 4, 16, sums)))) return rc;
     const hipStream_t cs = mode != 0 ? c->rs : c->cs;
+    // mode 3: the copy in halves on two engines when two are free (r05, tools/copy_ab.py: 49.3 vs 50.3 us per
+    // pipelined c2 GRAY8 frame), each half decrementing sd_done.  (Rendering a synchronous frame in two row chunks,
+    // each copied as soon as it is in its buffer, measured no faster: 83.9 vs 83.1 us — the chunks are two views to
+    // the per-view tile-order and cone caches, and each copy's start after its signal costs ~8 us.)
+    const size_t nbytes = npx * pb;
+    const size_t half = c->sd_engine2 && c->sd_split >= 2 && nbytes >= 65536 ? nbytes / 2 & ~(size_t)255 : 0;
     if (mode == 3) {                                    // before the render is queued: it fires sd_dep
         hsa_signal_store_relaxed(c->sd_dep[slot], 1);
-        hsa_signal_store_relaxed(c->sd_done[slot], 1);
+        hsa_signal_store_relaxed(c->sd_done[slot], half ? 2 : 1);
     }
     // the slot's device buffer is free once its previous frame's copy has left (ordered by the stream when that
     // copy ran on the render stream)
@@ -1280,13 +1290,23 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
     if (mode == 3) {
         RT_HIP(sdma_fire(c, slot, c->sd_writer));      // the frame is in px
         const hsa_status_t hs = hsa_amd_memory_async_copy_on_engine(
-            host, c->sd_cpu, px, c->sd_gpu, npx * pb, 1, &c->sd_dep[slot], c->sd_done[slot],
+            host, c->sd_cpu, px, c->sd_gpu, half ? half : nbytes, 1, &c->sd_dep[slot], c->sd_done[slot],
             (hsa_amd_sdma_engine_id_t)c->sd_engine, true);
         if (hs != HSA_STATUS_SUCCESS) {
             RT_HIP(hipStreamSynchronize(c->rs));
             return rt_fail(RT_EHIP, "rt_render_packed: hsa_amd_memory_async_copy_on_engine failed");
         }
-        c->sd_pending[slot] = true;
+        c->sd_pending[slot] = true;                     // (the first copy is queued: its slot must be waited for)
+        if (half) {
+            const hsa_status_t h2 = hsa_amd_memory_async_copy_on_engine(
+                (char*)host + half, c->sd_cpu, (char*)px + half, c->sd_gpu, nbytes - half, 1, &c->sd_dep[slot],
+                c->sd_done[slot], (hsa_amd_sdma_engine_id_t)c->sd_engine2, true);
+            if (h2 != HSA_STATUS_SUCCESS) {
+                hsa_signal_subtract_screlease(c->sd_done[slot], 1);   // the half that was not queued
+                (void)sdma_wait(c, slot);
+                return rt_fail(RT_EHIP, "rt_render_packed: hsa_amd_memory_async_copy_on_engine failed");
+            }
+        }
         c->copied_rec[slot] = false;
         return RT_OK;
     }

@@ -88,13 +88,30 @@ int main() {
         while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE) != 0) {}
     }});
     for (int k = 0; k < 16; ++k) {
-        if (!(mask & (1u << k))) continue;
+        if (!(mask & (1u << k)) || k >= (getenv("ENGINES") ? atoi(getenv("ENGINES")) : 16)) continue;
         const hsa_amd_sdma_engine_id_t eng = (hsa_amd_sdma_engine_id_t)(1u << k);
         cases.push_back({"sdma" + std::to_string(k), [&, eng] {
             hsa_signal_store_relaxed(sig, 1);
             HK(hsa_amd_memory_async_copy_on_engine(h_dst, g_cpu, d_src, g_gpu, n, 0, nullptr, sig, eng, true));
             while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE) != 0) {}
         }});
+    }
+    // the frame in halves on two engines at once (one completion signal counting both): does PCIe take more than one
+    // engine's rate?
+    {
+        int e0 = -1, e1 = -1;
+        for (int k = 0; k < 16; ++k)
+            if (mask & (1u << k)) { if (e0 < 0) e0 = k; else if (e1 < 0) e1 = k; }
+        if (e1 >= 0) {
+            const hsa_amd_sdma_engine_id_t a = (hsa_amd_sdma_engine_id_t)(1u << e0), b = (hsa_amd_sdma_engine_id_t)(1u << e1);
+            cases.push_back({"sdma" + std::to_string(e0) + "+" + std::to_string(e1) + "_halves", [&, a, b] {
+                hsa_signal_store_relaxed(sig, 2);
+                HK(hsa_amd_memory_async_copy_on_engine(h_dst, g_cpu, d_src, g_gpu, n / 2, 0, nullptr, sig, a, true));
+                HK(hsa_amd_memory_async_copy_on_engine((char*)h_dst + n / 2, g_cpu, (char*)d_src + n / 2, g_gpu, n - n / 2,
+                                                       0, nullptr, sig, b, true));
+                while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE) != 0) {}
+            }});
+        }
     }
     // busy kernel alone
     const int iters = getenv("ITERS") ? atoi(getenv("ITERS")) : 20000;

@@ -12,7 +12,7 @@ for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
   d=$ROOT/tools/_var/$name; mkdir -p "$d"
   echo $UNITS | tr ' ' '\n' | (cd "$SRC" && xargs -P 8 -I{} /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off \
-      -fno-fast-math -Wall -Wno-unused-function --offload-arch=gfx950 -mllvm -amdgpu-kernarg-preload-count=${KERNARG_PRELOAD:-0} -DRT_MAX_B=${RT_MAX_B:-3} $flags -c {}.hip -o "$d/{}.o")
+      -fno-fast-math -Wall -Wno-unused-function --offload-arch=gfx950 ${KERNARG_PRELOAD:+-mllvm -amdgpu-kernarg-preload-count=$KERNARG_PRELOAD} -DRT_MAX_B=${RT_MAX_B:-3} $flags -c {}.hip -o "$d/{}.o")
   objs=$(for u in $UNITS; do echo "$d/$u.o"; done)
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$d/librt_amd.so" $objs "$LIB/rt_host.o" "$LIB/rt_screen.o" \
       "$LIB/rt_group.o" "$LIB/rt_group_plan.o" -L/opt/rocm/lib -lrccl -lhsa-runtime64
