@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -1224,8 +1225,15 @@ static bool sdma_init(rt_ctx* c) {
 // the engine is not left waiting, and reported.
 static int sdma_wait(rt_ctx* c, int b) {
     if (!c->sd_pending[b]) return RT_OK;
-    const hsa_signal_value_t v = hsa_signal_wait_scacquire(c->sd_done[b], HSA_SIGNAL_CONDITION_LT, 1,
-                                                           (uint64_t)5e9, HSA_WAIT_STATE_BLOCKED);
+    // (the wait's timeout is a hint in timestamp ticks and may return early: the deadline is kept here)
+    uint64_t freq = 0;
+    if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &freq) != HSA_STATUS_SUCCESS || freq == 0) freq = 1000000000;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(5);
+    hsa_signal_value_t v = 1;
+    while ((v = hsa_signal_wait_scacquire(c->sd_done[b], HSA_SIGNAL_CONDITION_LT, 1, freq / 10,
+                                          HSA_WAIT_STATE_BLOCKED)) >= 1 &&
+           std::chrono::steady_clock::now() < deadline) {
+    }
     c->sd_pending[b] = false;
     if (v < 1) return RT_OK;
     hsa_signal_store_screlease(c->sd_dep[b], 0);
