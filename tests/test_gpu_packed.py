@@ -365,6 +365,43 @@ def test_render_packed_two_behind_and_mixed_sync(tr, monkeypatch, copy_mode):
         t.close()
 
 
+@pytest.mark.parametrize("split", ["1", "2"])
+def test_render_packed_sdma_one_or_two_engines(tr, monkeypatch, split):
+    """The SDMA path with the frame copied whole by one engine (RT_SDMA_SPLIT=1, or a frame under 64 KiB) or in
+    halves by two: synchronous and pipelined frames equal the device render, byte for byte."""
+    monkeypatch.setenv("RT_COPY_MODE", "3")
+    monkeypatch.setenv("RT_SDMA_SPLIT", split)
+    L = abi.lib()
+    cfg = scenes.CONFIGS["c2"]
+    sa = cfg.scene().to_abi()
+    tr.set_scene(cfg.scene())
+    t = Tracer(0)
+    try:
+        for W, H in ((64, 48), (640, 360)):              # 3 KB (one piece whatever the split) and 230 KB
+            cam = cfg.camera(W, H)
+            want = _rgba(tr, cam, W, H, cfg.depth)[1].cpu().numpy()[..., 0]
+            pins = [_host_alloc(W * H) for _ in range(3)]
+            try:
+                abi.check(L.rt_render_packed(t._ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, cfg.depth,
+                                             P.RT_PIXEL_GRAY8, pins[0], None), "rt_render_packed")
+                assert _copy_path(t)[0] == 3
+                got = np.ctypeslib.as_array(ctypes.cast(pins[0], ctypes.POINTER(ctypes.c_uint8)), (H, W))
+                assert np.array_equal(got, want), (W, H)
+                tk = [ctypes.c_uint64() for _ in range(3)]
+                for f in range(6):
+                    abi.check(L.rt_render_packed_async(t._ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, cfg.depth,
+                                                       P.RT_PIXEL_GRAY8, pins[f % 3], ctypes.byref(tk[f % 3])), "async")
+                abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
+                for j in range(3):
+                    got = np.ctypeslib.as_array(ctypes.cast(pins[j], ctypes.POINTER(ctypes.c_uint8)), (H, W))
+                    assert np.array_equal(got, want), (W, H, j)
+            finally:
+                for p in pins:
+                    L.rt_host_free(p)
+    finally:
+        t.close()
+
+
 def test_hits_inside_shortcut_far_origins(tr):
     """Rays from hit points skip the bounding-sphere cull only when the host proved every hit point lies inside
     its shortcut radius with a slack that covers the hit point's rounding, which grows with the level-0 origin's
