@@ -1,4 +1,4 @@
-"""GPU tests of the per-view primary cone-mask cache (rt_kernel.hip render_dev_impl, rt_cone_permute_kernel):
+"""GPU tests of the per-view primary cone-mask cache (rt_kernel.hip render_dev_impl, rt_disp_kernel):
 the calibration render of a static view records each 8x8 tile's primary-ray sphere mask, later renders of
 exactly that view read it (one scalar load) instead of recomputing it, and renders of any other camera
 compute their own.  The masks only skip spheres a tile's rays provably miss, so every frame must stay
@@ -48,6 +48,24 @@ def test_static_view_frames_hash_to_the_reference(tr, name):
         b = tr.render(cfg.camera(), cfg.width, cfg.height, cfg.depth, rgba32f=False, rgb64f=True)
         torch.cuda.synchronize()
         assert _hash(b) == want, f"render {k}"
+
+
+@pytest.mark.parametrize("name", ["c2", "c5"])
+def test_tile_order_policy_frames_hash_to_the_reference(monkeypatch, name):
+    """The per-tile longest-first dispatch order (RT_ORDER_POLICY=1: tile costs sorted by hipCUB into the dispatch
+    records) instead of the tile-row order: the first, calibration and cached renders all hash to the reference."""
+    monkeypatch.setenv("RT_ORDER_POLICY", "1")
+    cfg = scenes.CONFIGS[name]
+    t = Tracer(0)
+    try:
+        t.set_scene(cfg.scene())
+        want = golden.manifest()["frames"][name]["fnv1a64"]
+        for k in range(4):
+            b = t.render(cfg.camera(), cfg.width, cfg.height, cfg.depth, rgba32f=False, rgb64f=True)
+            torch.cuda.synchronize()
+            assert _hash(b) == want, f"render {k}"
+    finally:
+        t.close()
 
 
 def test_other_cameras_and_back(tr):
