@@ -61,7 +61,7 @@ if want hostw; then
 fi
 if want refill; then
   for c in ${REFILL_CONFIGS:-c5 c2}; do
-    gx=960; case "$c" in c2*) gx=240;; esac
+    gx=960; case "$c" in c2pair) gx=120;; c5pair) gx=480;; c2*) gx=240;; esac
     timeout -k 10 120 ./tools/_var/mb_refill $c $gx >> "$OUT/refill.jsonl" 2> "$OUT/refill.err" \
         || { echo "refill $c failed"; tail -20 "$OUT/refill.err"; exit 24; }
   done
