@@ -1265,8 +1265,10 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
     // RT_COPY_MODE=2 (A/B): the kernel stores the frame straight into the pinned host buffer (mapped into the
     // device's address space), no device buffer and no copy; 3: an SDMA engine copies it (rt_ctx sd_*)
     int mode = c->copy_mode >= 0 ? c->copy_mode : (async ? 3 : 1);
-    // (the engine needs page-locked host memory: pageable buffers take the copy-kernel / hipMemcpyAsync path)
-    if (mode == 3 && (!host_device_ptr(host, npx * pb) || !sdma_init(c))) mode = async ? 0 : 1;
+    // (the engine needs page-locked host memory: pageable buffers take the copy-kernel / hipMemcpyAsync path; it is
+    // given the buffer's device-side address, which for memory registered after allocation may differ from `host`)
+    void* const hdev = mode == 3 ? host_device_ptr(host, npx * pb) : nullptr;
+    if (mode == 3 && (!hdev || !sdma_init(c))) mode = async ? 0 : 1;
     // the slot's device buffer: an SDMA copy of an earlier frame may still read it (whatever this call's mode)
     if ((rc = sdma_wait(c, slot))) return rc;
     c->last_copy_mode = mode;
@@ -1298,7 +1300,7 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
     if (mode == 3) {
         RT_HIP(sdma_fire(c, slot, c->sd_writer));      // the frame is in px
         const hsa_status_t hs = hsa_amd_memory_async_copy_on_engine(
-            host, c->sd_cpu, px, c->sd_gpu, half ? half : nbytes, 1, &c->sd_dep[slot], c->sd_done[slot],
+            hdev, c->sd_cpu, px, c->sd_gpu, half ? half : nbytes, 1, &c->sd_dep[slot], c->sd_done[slot],
             (hsa_amd_sdma_engine_id_t)c->sd_engine, true);
         if (hs != HSA_STATUS_SUCCESS) {
             RT_HIP(hipStreamSynchronize(c->rs));
@@ -1307,7 +1309,7 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
         c->sd_pending[slot] = true;                     // (the first copy is queued: its slot must be waited for)
         if (half) {
             const hsa_status_t h2 = hsa_amd_memory_async_copy_on_engine(
-                (char*)host + half, c->sd_cpu, (char*)px + half, c->sd_gpu, nbytes - half, 1, &c->sd_dep[slot],
+                (char*)hdev + half, c->sd_cpu, (char*)px + half, c->sd_gpu, nbytes - half, 1, &c->sd_dep[slot],
                 c->sd_done[slot], (hsa_amd_sdma_engine_id_t)c->sd_engine2, true);
             if (h2 != HSA_STATUS_SUCCESS) {
                 hsa_signal_subtract_screlease(c->sd_done[slot], 1);   // the half that was not queued

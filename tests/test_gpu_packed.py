@@ -402,6 +402,45 @@ def test_render_packed_sdma_one_or_two_engines(tr, monkeypatch, split):
         t.close()
 
 
+def test_render_packed_sdma_into_registered_memory(tr, monkeypatch):
+    """Host memory the caller page-locked after allocating it (hipHostRegister) is reached by the SDMA engines at its
+    device-side address: synchronous and pipelined frames into it equal the device render."""
+    cudart = torch.cuda.cudart()
+    if not hasattr(cudart, "cudaHostRegister"):
+        pytest.skip("no host-register binding in this torch")
+    monkeypatch.setenv("RT_COPY_MODE", "3")
+    L = abi.lib()
+    cfg = scenes.CONFIGS["c2"]
+    sa = cfg.scene().to_abi()
+    W, H = 640, 360
+    cam = cfg.camera(W, H)
+    tr.set_scene(cfg.scene())
+    want = _rgba(tr, cam, W, H, cfg.depth)[1].cpu().numpy()[..., 0]
+    bufs = [np.zeros((H, W), np.uint8) for _ in range(3)]
+    for b in bufs:
+        assert int(cudart.cudaHostRegister(b.ctypes.data, b.nbytes, 0)) == 0
+    t = Tracer(0)
+    try:
+        abi.check(L.rt_render_packed(t._ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, cfg.depth, P.RT_PIXEL_GRAY8,
+                                     ctypes.c_void_p(bufs[0].ctypes.data), None), "rt_render_packed")
+        assert _copy_path(t)[0] == 3
+        assert np.array_equal(bufs[0], want)
+        for b in bufs:
+            b[:] = 0
+        tk = [ctypes.c_uint64() for _ in range(3)]
+        for f in range(6):
+            abi.check(L.rt_render_packed_async(t._ctx, ctypes.byref(sa), ctypes.byref(cam), W, H, cfg.depth,
+                                               P.RT_PIXEL_GRAY8, ctypes.c_void_p(bufs[f % 3].ctypes.data),
+                                               ctypes.byref(tk[f % 3])), "async")
+        abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
+        for b in bufs:
+            assert np.array_equal(b, want)
+    finally:
+        t.close()
+        for b in bufs:
+            cudart.cudaHostUnregister(b.ctypes.data)
+
+
 def test_hits_inside_shortcut_far_origins(tr):
     """Rays from hit points skip the bounding-sphere cull only when the host proved every hit point lies inside
     its shortcut radius with a slack that covers the hit point's rounding, which grows with the level-0 origin's
