@@ -159,9 +159,6 @@ struct RenderParams {
     int32_t ns;                                // stride of the scene's per-sphere arrays (DevScene::n_stride)
 };
 
-// The render kernels' arguments, in order: the kernel-argument segment lays them out as this struct (each at its
-// natural alignment), which late_outputs() relies on.  (The kernels take them as separate parameters: one
-// by-value struct parameter measured +11 VGPRs in the culling kernel.)
 // The dispatch table's geometry, scalar arguments right after the table, so that gfx950's kernarg preload
 // (-mllvm -amdgpu-kernarg-preload-count=4, Makefile KERNARG_PRELOAD) can hand both to the wave in SGPRs and its
 // first memory access is its dispatch record.  Measured (r05, tools/ab_libs.py, 9 rounds): preloading 4 or 6
@@ -171,6 +168,9 @@ struct DispGeom {
     int32_t n;                                 // dispatch positions with a record (tile rows x tiles_x)
 };
 
+// The render kernels' arguments, in order: the kernel-argument segment lays them out as this struct (each at its
+// natural alignment), which late_outputs() relies on.  (The kernels take them as separate parameters: one
+// by-value struct parameter measured +11 VGPRs in the culling kernel.)
 struct RenderArgs {
     const DispRec* disp;                       // dispatch table (nullptr: identity order)
     int32_t tiles_x, n_disp;                   // its DispGeom (scalars: aggregates are not preloaded)
