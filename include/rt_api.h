@@ -229,7 +229,8 @@ int rt_pixel_bytes(int format, int* bytes);
  * specular, transparency of the board squares when the board is present, of the sphere material when there
  * are spheres, of the tetrahedron / cube materials when such meshes are present) and every light colour has
  * three equal components (MySdlApplication.cpp:577, 583-588: the app's board, spheres and tetrahedron are; its
- * red cube is not).  Host only. */
+ * red cube is not).  Host only.  (The renders use the same test, with no transparent material, to run one-channel
+ * kernel instances whose three channels are bitwise equal by construction.) */
 int rt_scene_achromatic(const rt_scene* scene, int* out);
 /* rt_render_dev with the float image in `float_format` (RT_PIXEL_RGBA32F / GRAY32F) and the byte image in
  * `byte_format` (RT_PIXEL_RGBA8 / RGB8 / GRAY8); each image nullable.  Same rules as rt_render_dev. */
