@@ -449,6 +449,20 @@ def cpu_sample(render, seconds):
     return blocks, max(blocks, key=lambda b: b[0] / b[1])
 
 
+def cpu_baseline_labels(nt, env=None):
+    """What the CPU sample ran on: `threads` = the OpenMP threads used — the lease's CPU share (OMP_NUM_THREADS, 16 on
+    the GPU boxes), hardware threads, not physical cores; `cores` repeats it because the bench contract names that key
+    (its meaning is `threads`, stated in `threads_note`); `nproc` and `affinity_threads` = the machine's hardware threads
+    and those this process may run on."""
+    env = os.environ if env is None else env
+    return {"unit": "Mray/s", "threads": nt, "cores": nt,
+            "threads_note": (f"{nt} OpenMP threads = the lease's CPU share (OMP_NUM_THREADS="
+                             f"{env.get('OMP_NUM_THREADS')}) of a {os.cpu_count()}-hardware-thread host; hardware "
+                             "threads, not physical cores ('cores' = the same count, the key the bench contract names)"),
+            "nproc": os.cpu_count(), "affinity_threads": affinity_cores(),
+            "omp_num_threads_env": env.get("OMP_NUM_THREADS"), "host_cpu": cpu_model()}
+
+
 def cpu_baseline(args, cfg, scene, cam, W, H, B, rays_frame):
     """The CPU path timed on this host (rank 0, N = 1): the reference's own rayTraceRay compiled from its sources
     (oracle/_ref/libref.so: built in the build container by oracle/Makefile, it travels with the tree; kind
@@ -466,9 +480,7 @@ def cpu_baseline(args, cfg, scene, cam, W, H, B, rays_frame):
         po.render(sa, cam, W, H, B, nthreads=1)
         n1 += 1
     per_core = rays_frame * n1 / (time.perf_counter() - t1) / 1e6
-    common = {"unit": "Mray/s", "cores": nt, "threads_used": nt, "nproc": os.cpu_count(),
-              "affinity_cores": affinity_cores(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
-              "host_cpu": cpu_model()}
+    common = cpu_baseline_labels(nt)
     port_desc = (f"oracle/rt_oracle.c (bit-exact restatement, gcc -O2 -ffp-contract=off -fopenmp, OpenMP {nt} threads, "
                  f"schedule(dynamic,1) over rows): best of 3 blocks of whole {cfg.name} frames "
                  f"({', '.join(str(b[0]) for b in pblocks)} frames in {', '.join(f'{b[1]:.1f}' for b in pblocks)} s)")

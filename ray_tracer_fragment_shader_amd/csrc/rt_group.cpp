@@ -93,6 +93,12 @@ struct rt_group {
     // RT_GATHER_ROOT_WAITS=1 (A/B): the root's receives / peer copies wait for the root's own render first (r03)
     bool root_waits = false;
     uint64_t last_payload = 0;
+    // the frame plans (rt_group_plan.cpp) of the local ranks and of rank 0, for the key {W, H, band_height, outputs,
+    // achromatic}: recomputed only when the key changes (no host allocation or per-rank loops per frame)
+    std::vector<rt_group_plan> plan;           // sized at creation: one per local rank
+    rt_group_plan root_plan{};
+    int plan_key[5] = {0, 0, 0, 0, 0};
+    bool plan_valid = false;
 };
 
 namespace {
@@ -224,6 +230,7 @@ extern "C" int rt_group_create(rt_ctx* const* ctxs, int n, int transport, rt_gro
     g->transport = transport;
     g->owns_root = true;
     g->ranks.resize(n);
+    g->plan.resize(n);
     int rc = RT_OK;
     // COPY: the root's comm stream records every rank's `sent` events, so they live on the root device.
     std::vector<hipEvent_t> root_sent(2 * n, nullptr);
@@ -265,6 +272,7 @@ extern "C" int rt_group_create_rank(rt_ctx* ctx, int n_ranks, int rank, const ui
     g->transport = RT_TRANSPORT_RCCL;
     g->owns_root = rank == 0;
     g->ranks.resize(1);
+    g->plan.resize(1);
     int rc = setup_rank(&g->ranks[0], ctx, rank, nullptr);
     if (rc == RT_OK && g->owns_root) rc = setup_root_events(g);
     if (rc == RT_OK) {
@@ -414,22 +422,35 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     const int b = (int)(g->frame & 1);
     const int slot = (int)(g->frame % kRing);
     const hipStream_t st = (hipStream_t)stream;
-    // Wire formats: every local rank must see the same scene (each decides from its own context).
+    // Every local rank must hold the same scene: the frame is assembled from their bands, and the wire formats are
+    // decided from rank 0's context.  The scene fingerprint (FNV-1a of the flattened record, the value the
+    // one-process-per-GPU groups all-reduce below) is compared, not just the achromatic flag.
     const int achro = rt_ctx_achromatic(g->ranks[0].ctx);
-    for (auto& r : g->ranks)
-        if (rt_ctx_achromatic(r.ctx) != achro)
+    uint64_t gen0 = 0, fp0 = 0;
+    rt_ctx_scene_id(g->ranks[0].ctx, &gen0, &fp0);
+    for (auto& r : g->ranks) {
+        uint64_t gen = 0, fp = 0;
+        rt_ctx_scene_id(r.ctx, &gen, &fp);
+        if (fp != fp0 || rt_ctx_achromatic(r.ctx) != achro)
             return rt_fail(RT_EINVAL, "rt_render_multi: the ranks' contexts hold different scenes");
+    }
     // ... and across the processes of a one-process-per-GPU group
     if (g->n_ranks > 1 && (int)g->ranks.size() < g->n_ranks && (rc = agree_on_scene(g, g->ranks[0], achro)))
         return rc;
     // What every rank sends and where rank 0's receives land: the host-only plan (rt_group_plan.cpp), one per local
     // rank, plus rank 0's (its receive table and payload) — the same plan the CPU tests check across processes.
-    std::vector<rt_group_plan> plan(g->ranks.size());
-    for (size_t q = 0; q < g->ranks.size(); ++q)
-        if ((rc = rt_group_plan_frame(W, H, g->n_ranks, g->ranks[q].rank, band_height, outputs, achro, &plan[q])))
-            return rc;
-    rt_group_plan root_plan;
-    if ((rc = rt_group_plan_frame(W, H, g->n_ranks, 0, band_height, outputs, achro, &root_plan))) return rc;
+    const int key[5] = {W, H, band_height, outputs, achro};
+    if (!g->plan_valid || memcmp(key, g->plan_key, sizeof(key)) != 0) {
+        g->plan_valid = false;
+        for (size_t q = 0; q < g->ranks.size(); ++q)
+            if ((rc = rt_group_plan_frame(W, H, g->n_ranks, g->ranks[q].rank, band_height, outputs, achro, &g->plan[q])))
+                return rc;
+        if ((rc = rt_group_plan_frame(W, H, g->n_ranks, 0, band_height, outputs, achro, &g->root_plan))) return rc;
+        memcpy(g->plan_key, key, sizeof(key));
+        g->plan_valid = true;
+    }
+    const std::vector<rt_group_plan>& plan = g->plan;
+    const rt_group_plan& root_plan = g->root_plan;
     const int hb = root_plan.band_height, slab_rows = root_plan.slab_rows;
     // (the render call takes a format for an image it does not write too)
     const int wire[kKinds] = {achro ? RT_PIXEL_GRAY32F : RT_PIXEL_RGBA32F, achro ? RT_PIXEL_GRAY8 : RT_PIXEL_RGB8};
@@ -493,7 +514,13 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
             if (kind_on[k] && (rc = grow(&g->gathered[b][k], &g->gathered_cap[b][k], root_plan.gather_bytes[k])))
                 return rc;
     }
-    std::vector<PhaseEvents*> pe(g->ranks.size(), nullptr);
+    PhaseEvents* pe_fixed[8] = {};             // (no allocation per frame for up to 8 local ranks)
+    std::vector<PhaseEvents*> pe_more;
+    PhaseEvents** pe = pe_fixed;
+    if (g->ranks.size() > 8) {
+        pe_more.assign(g->ranks.size(), nullptr);
+        pe = pe_more.data();
+    }
     if (g->timing)
         for (size_t q = 0; q < g->ranks.size(); ++q)
             if ((rc = phase_events(g->ranks[q], slot, q == 0 && g->owns_root, &pe[q]))) return rc;
@@ -618,8 +645,8 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         G_HIP(hipStreamWaitEvent(st, g->assembled[b], 0));
         g->assembled_rec[b] = true;
     }
-    for (auto* e : pe)
-        if (e) e->rec = true;
+    for (size_t q = 0; q < g->ranks.size(); ++q)
+        if (pe[q]) pe[q]->rec = true;
     ++g->frame;
     return RT_OK;
 }

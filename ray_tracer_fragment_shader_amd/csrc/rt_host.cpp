@@ -357,8 +357,9 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
     put(d->bc, bc);
     d->br2 = s->radius * s->radius;                                             // :750
     d->bound_on = s->radius > 0;                                                // :747 (g_scene is not _amSphere)
-    // origins with |o - bc|^2 < (R-1)^2 provably pass the cull (proof at rt_device.hpp bound_pass_dp)
-    d->inner2 = s->radius > 2 ? (s->radius - 1) * (s->radius - 1) : -1.0;
+    // origins with |o - bc|^2 < (R-1)^2 provably pass the cull (proof at rt_device.hpp bound_pass_dp: |s| >= 1, which
+    // clears the reference's |s| < SMALL_NUMBER test only while SMALL_NUMBER < 1 — kept below 0.5 for the rounding)
+    d->inner2 = s->radius > 2 && s->small_number < 0.5 ? (s->radius - 1) * (s->radius - 1) : -1.0;
     d->eps = s->small_number;
     d->att = s->attenuation_factor;
     put(d->coff, bc);                                                           // CheckerBoard's positionOffset
@@ -532,7 +533,7 @@ int rt_build_dev_scene(const rt_scene* s, std::vector<unsigned char>* blob) {
         const double radius = std::sqrt((double)3) * M.edge / 2;
         put(DM.bc, mpos);
         DM.br2 = radius * radius;
-        DM.inner2 = radius > 2 ? (radius - 1) * (radius - 1) : -1.0;
+        DM.inner2 = radius > 2 && s->small_number < 0.5 ? (radius - 1) * (radius - 1) : -1.0;   // (as g_scene's)
         DM.tri0 = t_next;
         DM.child = (s->has_board ? 1 : 0) + M.after_spheres + m;
         const double h = M.edge / 2;

@@ -151,11 +151,12 @@ __global__ __launch_bounds__(kThreads) void rt_prepare_kernel(DevScene* __restri
         // (hits_inside) and the eye is at least R + 1 away: the line then passes within R - 1 of bc, so its exact
         // disc >= R^2 - (R - 1)^2 = 2R - 1, and the eye being outside the bound puts the entry root at
         // s >= D - R >= 1 (the hit lies ahead of the eye, past the entry); the FP64 rounding of disc and s is
-        // ~2^-49 (D^2 + R^2) and ~2^-50 (D + R), far below 2R - 1 and 1 - eps for D <= 2^20 (R + 1).
+        // ~2^-49 (D^2 + R^2) and ~2^-50 (D + R), far below 2R - 1 and 1 - eps for D <= 2^20 (R + 1).  (s >= 1 clears the
+        // reference's |s| < eps cull only for eps < 1: required explicitly, as hits_inside does through inner2.)
         const double bx = eye.x - g->bc[0], by = eye.y - g->bc[1], bz = eye.z - g->bc[2];
         const double D2 = bx * bx + by * by + bz * bz, R1 = sqrt(g->br2) + 1.0;
-        g->prim_bound_ok = (g->bound_on != 0) & (g->hits_inside != 0) & (D2 >= R1 * R1 * (1.0 + 0x1p-30)) &
-                           (D2 <= R1 * R1 * 0x1p40);
+        g->prim_bound_ok = (g->bound_on != 0) & (g->hits_inside != 0) & (g->eps < 0.5) &
+                           (D2 >= R1 * R1 * (1.0 + 0x1p-30)) & (D2 <= R1 * R1 * 0x1p40);
     }
     if (k >= np) return;
     d3 dP = sub(ld3(sph[k].c), eye);
@@ -516,15 +517,20 @@ struct rt_ctx {
     bool copied_cs[kSlots] = {};               // ... by a copy on the copy stream (else on the render stream)
     // copy_mode 3: the frame leaves on a copy (SDMA) engine — no CUs taken from the next render.  Per slot, the
     // render stream stores 0 into sd_dep (hipStreamWriteValue64 on the HSA signal's value) once the frame is in its
-    // device buffer; the SDMA copy, queued with sd_dep as its dependency, then moves it and decrements sd_done.
+    // device buffer; the SDMA copies, queued with sd_dep as their dependency, then move it, each decrementing its
+    // own completion signal sd_done[slot][half] (one signal per engine copy, initialised to 1).
     bool sd_tried = false, sd_ok = false;
     hsa_agent_t sd_gpu{0}, sd_cpu{0};
     uint32_t sd_engine = 0, sd_engine2 = 0;            // the two lowest free engines (sd_engine2 = 0: only one)
     int sd_split = 2;                                   // RT_SDMA_SPLIT: engines a frame's copy is split over (1, 2)
-    hsa_signal_t sd_dep[kSlots] = {}, sd_done[kSlots] = {};
+    hsa_signal_t sd_dep[kSlots] = {}, sd_done[kSlots][2] = {};
     volatile hsa_signal_value_t* sd_dep_ptr[kSlots] = {};
+    hipEvent_t sd_fired[kSlots] = {};                   // recorded on rs right after slot b's sdma_fire
     bool sd_pending[kSlots] = {};
+    int sd_copies[kSlots] = {};                         // engine copies queued for slot b (1 or 2)
     int sd_writer = 0;                                  // sdma_fire: 1 stream write-value, 2 signal kernel
+    int sd_writer_req = 0;                              // RT_SDMA_WRITER (A/B): 1 or 2 forces the writer, 0 tries 1 then 2
+    int sd_wait_ms = 5000;                              // RT_SDMA_WAIT_MS: how often sdma_wait re-checks a slow render
     int last_copy_mode = -1;                            // the mode the last packed frame took (rt_diag_copy_path)
     uint64_t ticket = 0;                       // rt_render_packed_async frames queued so far
     // rt_render's device buffers (grow-only, reused across calls): rgba32f, rgba8, rgb64f, raycount, sums,
@@ -629,7 +635,9 @@ extern "C" int rt_ctx_destroy(rt_ctx* c) {
         for (int b = 0; b < rt_ctx::kSlots; ++b) {
             (void)sdma_wait(c, b);                     // (the render stream has drained: its signal has fired)
             hsa_signal_destroy(c->sd_dep[b]);
-            hsa_signal_destroy(c->sd_done[b]);
+            hsa_signal_destroy(c->sd_done[b][0]);
+            hsa_signal_destroy(c->sd_done[b][1]);
+            (void)hipEventDestroy(c->sd_fired[b]);
         }
         hsa_shut_down();
     }
@@ -664,6 +672,8 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_TILE_ORDER")) c->order_mode = atoi(e) == 1 ? 1 : 0;   // 1: bottom-to-top (A/B)
     if (const char* e = getenv("RT_COPY_MODE")) c->copy_mode = std::min(std::max(atoi(e), -1), 3);
     if (const char* e = getenv("RT_SDMA_SPLIT")) c->sd_split = std::min(std::max(atoi(e), 1), 2);
+    if (const char* e = getenv("RT_SDMA_WRITER")) c->sd_writer_req = std::min(std::max(atoi(e), 0), 2);
+    if (const char* e = getenv("RT_SDMA_WAIT_MS")) c->sd_wait_ms = std::max(atoi(e), 0);
     if (const char* e = getenv("RT_COPY_BLOCKS")) c->copy_blocks = std::max(atoi(e), 0);
     if (const char* e = getenv("RT_COPY_KERNEL")) c->copy_kernel = std::min(std::max(atoi(e), -1), 1);
     if (const char* e = getenv("RT_CONE_CACHE")) c->cone_cache = atoi(e) != 0;
@@ -1189,13 +1199,16 @@ static bool sdma_init(rt_ctx* c) {
     bool ok = true;
     for (int k = 0; k < rt_ctx::kSlots && ok; ++k)
         ok = hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &c->sd_dep[k]) == HSA_STATUS_SUCCESS &&
-             hsa_signal_create(0, 0, nullptr, &c->sd_done[k]) == HSA_STATUS_SUCCESS &&
-             hsa_amd_signal_value_pointer(c->sd_dep[k], &c->sd_dep_ptr[k]) == HSA_STATUS_SUCCESS;
+             hsa_signal_create(0, 0, nullptr, &c->sd_done[k][0]) == HSA_STATUS_SUCCESS &&
+             hsa_signal_create(0, 0, nullptr, &c->sd_done[k][1]) == HSA_STATUS_SUCCESS &&
+             hsa_amd_signal_value_pointer(c->sd_dep[k], &c->sd_dep_ptr[k]) == HSA_STATUS_SUCCESS &&
+             hipEventCreateWithFlags(&c->sd_fired[k], hipEventDisableTiming) == hipSuccess;
     // how the render stream fires it: the stream's own write (hipStreamWriteValue64), else a one-wave kernel's
     // system-scope store; each is tried once on slot 0's signal and must be seen from the host
     if (ok) {
         c->sd_writer = 0;
         for (int w = 1; w <= 2 && !c->sd_writer; ++w) {
+            if (c->sd_writer_req && w != c->sd_writer_req) continue;
             hsa_signal_store_screlease(c->sd_dep[0], 1);
             if (sdma_fire(c, 0, w) == hipSuccess && hipStreamSynchronize(c->rs) == hipSuccess &&
                 hsa_signal_load_scacquire(c->sd_dep[0]) == 0)
@@ -1207,7 +1220,10 @@ static bool sdma_init(rt_ctx* c) {
     if (!ok) {
         for (int k = 0; k < rt_ctx::kSlots; ++k) {
             if (c->sd_dep[k].handle) hsa_signal_destroy(c->sd_dep[k]);
-            if (c->sd_done[k].handle) hsa_signal_destroy(c->sd_done[k]);
+            for (int h = 0; h < 2; ++h)
+                if (c->sd_done[k][h].handle) hsa_signal_destroy(c->sd_done[k][h]);
+            if (c->sd_fired[k]) (void)hipEventDestroy(c->sd_fired[k]);
+            c->sd_fired[k] = nullptr;
         }
         hsa_shut_down();
         return false;
@@ -1221,24 +1237,51 @@ static bool sdma_init(rt_ctx* c) {
     return true;
 }
 
-// Wait until slot b's SDMA copy is done.  A dependency that never fired (its render failed) is released after 5 s so
-// the engine is not left waiting, and reported.
+// Wait until slot b's SDMA copies are done.  Elapsed time alone is not a failure: a deep frame may still be queued
+// behind others on the render stream.  Every sd_wait_ms the render stream's progress is checked (sd_fired, recorded
+// right after the frame's sdma_fire): while that event is pending the render is running, and once it has completed the
+// dependency has fired and the engines finish the copy — both keep waiting.  Only a render stream that reports an
+// error (its write never comes) has its dependency released by hand, so the engines are not left waiting; the stream
+// is then drained before the slot is reused, so no stale write of this frame can release a later frame's copy early.
 static int sdma_wait(rt_ctx* c, int b) {
     if (!c->sd_pending[b]) return RT_OK;
     // (the wait's timeout is a hint in timestamp ticks and may return early: the deadline is kept here)
     uint64_t freq = 0;
     if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &freq) != HSA_STATUS_SUCCESS || freq == 0) freq = 1000000000;
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(5);
-    hsa_signal_value_t v = 1;
-    while ((v = hsa_signal_wait_scacquire(c->sd_done[b], HSA_SIGNAL_CONDITION_LT, 1, freq / 10,
-                                          HSA_WAIT_STATE_BLOCKED)) >= 1 &&
-           std::chrono::steady_clock::now() < deadline) {
+    const auto period = std::chrono::milliseconds(c->sd_wait_ms);
+    auto done_by = [&](std::chrono::steady_clock::time_point deadline) {
+        for (int h = 0; h < c->sd_copies[b]; ++h) {
+            hsa_signal_value_t v = 1;
+            for (;;) {
+                // the wait's hint: at most 100 ms and no later than the deadline (0 at RT_SDMA_WAIT_MS=0: a poll)
+                const auto left = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                    deadline - std::chrono::steady_clock::now()).count();
+                const uint64_t hint = left <= 0 ? 0 : std::min<uint64_t>(freq / 10, (uint64_t)((double)left * 1e-9 * freq));
+                v = hsa_signal_wait_scacquire(c->sd_done[b][h], HSA_SIGNAL_CONDITION_LT, 1, hint, HSA_WAIT_STATE_BLOCKED);
+                if (v < 1 || std::chrono::steady_clock::now() >= deadline) break;
+            }
+            if (v >= 1) return false;
+        }
+        return true;
+    };
+    hipError_t q = hipSuccess;
+    for (;;) {
+        if (done_by(std::chrono::steady_clock::now() + period)) {
+            c->sd_pending[b] = false;
+            return RT_OK;
+        }
+        q = hipEventQuery(c->sd_fired[b]);
+        if (q != hipSuccess && q != hipErrorNotReady) break;       // the render stream failed
     }
-    c->sd_pending[b] = false;
-    if (v < 1) return RT_OK;
+    (void)hipGetLastError();
     hsa_signal_store_screlease(c->sd_dep[b], 0);
-    hsa_signal_wait_scacquire(c->sd_done[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
-    return rt_fail(RT_EHIP, "rt_render_packed: the frame's SDMA copy did not start within 5 s (render failed?)");
+    for (int h = 0; h < c->sd_copies[b]; ++h)
+        hsa_signal_wait_scacquire(c->sd_done[b][h], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+    (void)hipStreamSynchronize(c->rs);
+    (void)hipGetLastError();
+    c->sd_pending[b] = false;
+    return rt_fail(RT_EHIP, std::string("rt_render_packed: the frame's render failed before its SDMA copy: ") +
+                                hipGetErrorString(q));
 }
 
 // rt_render_packed / rt_render_packed_async: one image in `format`, copied to host memory.
@@ -1285,7 +1328,8 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
     const size_t half = c->sd_engine2 && c->sd_split >= 2 && nbytes >= 65536 ? nbytes / 2 & ~(size_t)255 : 0;
     if (mode == 3) {                                    // before the render is queued: it fires sd_dep
         hsa_signal_store_relaxed(c->sd_dep[slot], 1);
-        hsa_signal_store_relaxed(c->sd_done[slot], half ? 2 : 1);
+        hsa_signal_store_relaxed(c->sd_done[slot][0], 1);
+        hsa_signal_store_relaxed(c->sd_done[slot][1], 1);
     }
     // the slot's device buffer is free once its previous frame's copy has left (ordered by the stream when that
     // copy ran on the render stream)
@@ -1299,23 +1343,25 @@ static int render_packed_queue(rt_ctx* c, const rt_scene* scene, const rt_camera
     if (with_stats && (rc = queue_raysum(c, npx, (uint32_t*)rcb, (unsigned long long*)*sums))) return rc;
     if (mode == 3) {
         RT_HIP(sdma_fire(c, slot, c->sd_writer));      // the frame is in px
+        RT_HIP(hipEventRecord(c->sd_fired[slot], c->rs));
         const hsa_status_t hs = hsa_amd_memory_async_copy_on_engine(
-            hdev, c->sd_cpu, px, c->sd_gpu, half ? half : nbytes, 1, &c->sd_dep[slot], c->sd_done[slot],
+            hdev, c->sd_cpu, px, c->sd_gpu, half ? half : nbytes, 1, &c->sd_dep[slot], c->sd_done[slot][0],
             (hsa_amd_sdma_engine_id_t)c->sd_engine, true);
         if (hs != HSA_STATUS_SUCCESS) {
             RT_HIP(hipStreamSynchronize(c->rs));
             return rt_fail(RT_EHIP, "rt_render_packed: hsa_amd_memory_async_copy_on_engine failed");
         }
         c->sd_pending[slot] = true;                     // (the first copy is queued: its slot must be waited for)
+        c->sd_copies[slot] = 1;
         if (half) {
             const hsa_status_t h2 = hsa_amd_memory_async_copy_on_engine(
                 (char*)hdev + half, c->sd_cpu, (char*)px + half, c->sd_gpu, nbytes - half, 1, &c->sd_dep[slot],
-                c->sd_done[slot], (hsa_amd_sdma_engine_id_t)c->sd_engine2, true);
+                c->sd_done[slot][1], (hsa_amd_sdma_engine_id_t)c->sd_engine2, true);
             if (h2 != HSA_STATUS_SUCCESS) {
-                hsa_signal_subtract_screlease(c->sd_done[slot], 1);   // the half that was not queued
                 (void)sdma_wait(c, slot);
                 return rt_fail(RT_EHIP, "rt_render_packed: hsa_amd_memory_async_copy_on_engine failed");
             }
+            c->sd_copies[slot] = 2;
         }
         c->copied_rec[slot] = false;
         return RT_OK;

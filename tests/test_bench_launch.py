@@ -119,3 +119,12 @@ def test_c4_scaling_keys():
     txt = bench.c4_parallelism_text(8, dict(k, value=947.8))
     assert "8 GPUs" in txt and "efficiency" in txt and str(k["speedup_vs_c3_1gpu"]) in txt
     assert bench.c4_parallelism_text(8, {"error": "x"}) == ""
+
+
+def test_cpu_baseline_labels_threads_not_cores():
+    """The CPU baseline names what it ran on: OpenMP threads of the lease's share, not physical cores."""
+    lab = bench.cpu_baseline_labels(16, env={"OMP_NUM_THREADS": "16"})
+    assert lab["threads"] == 16 and lab["cores"] == lab["threads"]
+    assert "not physical cores" in lab["threads_note"] and "OMP_NUM_THREADS=16" in lab["threads_note"]
+    assert lab["nproc"] == os.cpu_count() and lab["affinity_threads"] >= 1
+    assert lab["omp_num_threads_env"] == "16" and "host_cpu" in lab and lab["unit"] == "Mray/s"

@@ -177,6 +177,45 @@ def test_group_errors_are_loud(tr):
         other.close()
 
 
+def test_render_multi_rejects_local_contexts_with_different_scenes(tr):
+    """A single-process group whose contexts hold different scenes — both achromatic, so the wire formats agree —
+    fails with RT_EINVAL instead of assembling a frame from two scenes (one g_scene per frame, MSA:590); once
+    both hold the same scene again the group renders the one-launch frame."""
+    L = abi.lib()
+    cfg = scenes.CONFIGS["c3"]
+    W, H = 320, 180
+    sc = cfg.scene()
+    other = cfg.scene()
+    other.spheres = other.spheres[:-1]                     # the same scene less its last sphere
+    for s in (sc, other):
+        flag = ctypes.c_int()
+        abi.check(L.rt_scene_achromatic(ctypes.byref(s.to_abi()), ctypes.byref(flag)), "rt_scene_achromatic")
+        assert flag.value == 1
+    ctxs = [Tracer(0) for _ in range(2)]
+    ctxs[0].set_scene(sc)
+    ctxs[1].set_scene(other)
+    g = _group(ctxs, abi.RT_TRANSPORT_COPY)
+    try:
+        cam = cfg.camera(W, H)
+        o8 = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+        s = torch.cuda.Stream()
+        rc = L.rt_render_multi(g, ctypes.byref(cam), W, H, cfg.depth, 0, abi.RT_OUT_RGBA8, None, _ptr(o8),
+                               ctypes.c_void_p(s.cuda_stream))
+        assert rc == abi.RT_EINVAL
+        assert "different scenes" in abi.last_error()
+        ctxs[1].set_scene(sc)
+        _multi(g, cam, W, H, cfg.depth, 0, None, o8, s)
+        s.synchronize()
+        tr.set_scene(sc)
+        want = tr.render(cam, W, H, cfg.depth, rgba32f=False, rgba8=True)["rgba8"]
+        torch.cuda.synchronize()
+        assert torch.equal(o8, want)
+    finally:
+        L.rt_group_destroy(g)
+        for c in ctxs:
+            c.close()
+
+
 def test_group_create_rank_one_process_per_gpu_path(tr):
     """The one-process-per-GPU constructor (rt_comm_unique_id + rt_group_create_rank, as bench.py uses under
     torch.distributed.run) with a one-rank communicator: same gather + assembly, equal to one launch."""

@@ -509,3 +509,49 @@ def test_host_frames_into_pinned_interior_pointers(tr, offset):
     finally:
         L.rt_host_free(base)
         t.close()
+
+
+@pytest.mark.parametrize("writer", ["1", "2"])
+def test_render_packed_sdma_slow_render_is_not_a_failure(tr, monkeypatch, writer):
+    """sdma_wait's progress check at RT_SDMA_WAIT_MS=0 (every wait passes its deadline at once): a render still
+    running when the deadline passes is waited for, not released by hand, so no copy starts before its frame is in its
+    buffer — pipelined frames two behind, alternating views, each equal to the device render.  Both writers of the
+    render stream's dependency store (the stream's write-value operation and the signal kernel, RT_SDMA_WRITER)."""
+    monkeypatch.setenv("RT_COPY_MODE", "3")
+    monkeypatch.setenv("RT_SDMA_WAIT_MS", "0")
+    monkeypatch.setenv("RT_SDMA_WRITER", writer)
+    L = abi.lib()
+    cfg = scenes.CONFIGS["c3"]
+    sa = cfg.scene().to_abi()
+    W, H = 1920, 1080
+    cams = [cfg.camera(W, H) for _ in range(3)]
+    cams[1].eye = abi.vec3((-40.0, 120.0, 230.0))
+    cams[2].eye = abi.vec3((35.0, 90.0, 210.0))
+    tr.set_scene(cfg.scene())
+    want = [_rgba(tr, c, W, H, cfg.depth)[1].cpu().numpy()[..., 0] for c in cams]
+    t = Tracer(0)
+    pins = [_host_alloc(W * H) for _ in range(3)]
+    try:
+        tickets = []
+        for f in range(12):
+            tk = ctypes.c_uint64()
+            abi.check(L.rt_render_packed_async(t._ctx, ctypes.byref(sa), ctypes.byref(cams[f % 3]), W, H, cfg.depth,
+                                               P.RT_PIXEL_GRAY8, pins[f % 3], ctypes.byref(tk)), "async")
+            tickets.append(tk.value)
+            if f >= 2:
+                abi.check(L.rt_ctx_wait(t._ctx, tickets[f - 2]), "rt_ctx_wait")
+                got = np.ctypeslib.as_array(ctypes.cast(pins[(f - 2) % 3], ctypes.POINTER(ctypes.c_uint8)), (H, W))
+                assert np.array_equal(got, want[(f - 2) % 3]), f - 2
+        assert _copy_path(t) == (3, int(writer))
+        abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
+        for f in (10, 11):
+            got = np.ctypeslib.as_array(ctypes.cast(pins[f % 3], ctypes.POINTER(ctypes.c_uint8)), (H, W))
+            assert np.array_equal(got, want[f % 3]), f
+        abi.check(L.rt_render_packed(t._ctx, ctypes.byref(sa), ctypes.byref(cams[1]), W, H, cfg.depth,
+                                     P.RT_PIXEL_GRAY8, pins[0], None), "rt_render_packed")
+        got = np.ctypeslib.as_array(ctypes.cast(pins[0], ctypes.POINTER(ctypes.c_uint8)), (H, W))
+        assert np.array_equal(got, want[1])
+    finally:
+        for p in pins:
+            L.rt_host_free(p)
+        t.close()

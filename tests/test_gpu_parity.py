@@ -773,6 +773,32 @@ def test_origin_skips_edge_cases(tr):
         assert np.array_equal(rc.cpu().numpy().view(np.uint32), want_rc), depth
 
 
+@pytest.mark.parametrize("name", ["c3", "c5", "demo"])
+@pytest.mark.parametrize("eps", [0.49, 1.0, 1.5, 12.0])
+def test_large_small_number_vs_oracle(tr, name, eps):
+    """SMALL_NUMBER (MSA:50) of 0.49 and at or above 1: the reference then culls bounding-sphere roots with
+    |s| < eps (:754) that the exact shortcuts prove to be >= 1 (inner2 for origins inside the bound, prim_bound_ok for
+    primary hits from an eye outside it), and misses sphere / board hits nearer than eps.  The shortcuts must stand
+    down above 0.5; frames and ray counts equal the oracle's bit for bit."""
+    cfg = scenes.CONFIGS[name]
+    W, H = 96, 72
+    sc = cfg.scene().to_abi()
+    sc.small_number = eps
+    rgb, rc = _render64(tr, sc, cfg.camera(W, H), W, H, cfg.depth)
+    want, want_rc = po.render(sc, cfg.camera(W, H), W, H, cfg.depth)
+    _assert_parity(rgb, want)
+    assert np.array_equal(rc, want_rc)
+    # rays from points inside the bounding sphere (the inner2 shortcut's domain) and from hit points
+    rng = np.random.default_rng(int(eps * 100))
+    n = 2048
+    s = np.stack([rng.uniform(-120, 120, n), rng.uniform(0.5, 60, n), rng.uniform(-300, -20, n)], axis=1)
+    e = s + rng.normal(size=(n, 3)) * 40.0
+    got, grc = tr.trace_rays(torch.tensor(s, device="cuda"), torch.tensor(e, device="cuda"), cfg.depth)
+    want, want_rc = po.trace_rays(sc, s, e, cfg.depth)
+    _assert_parity(got.cpu().numpy(), want)
+    assert np.array_equal(grc.cpu().numpy().view(np.uint32), want_rc)
+
+
 def test_render_kernels_do_not_spill(tr):
     """The render kernels the benchmark configs launch keep everything in registers (private scratch would
     be written back to HBM: PMC showed 1.2x the algorithmic write bytes when the r02 bounce loop spilled 36 B/lane),

@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Why the bench's one-rank c4 frame (rt_render_multi, 0.1332 ms in BENCH_r05) is slower than the same job's serial c3
+frame (0.1163 ms) while tools/c4_n1_probe.py, which keeps the GPU busy between modes, measures them equal; and what
+one GPU says about an 8-rank c4 frame.
+
+Part 1 (cold vs settled): the bench's group-leg procedure (20 untimed frames, 40 timed by the wall clock) started
+after the GPU idled for IDLE_S seconds, against the same procedure after SETTLE_S seconds of back-to-back frames.
+Modes: the one-rank group on the null stream (the bench), on a non-blocking stream, and plain rt_render_dev.
+
+Part 2 (N-rank projection): for N in 2, 4, 8, each rank's band set (rt_rows(hb, N, r)) rendered alone as GRAY8 into
+its slab, back to back on one stream and alternating over two streams (frames of the same rank overlapping), and
+rank 0's rt_unpack_dev of an N-rank gathered GRAY8 buffer into the RGBA8 image.  Prints JSON lines."""
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from ray_tracer_fragment_shader_amd import abi, scenes  # noqa: E402
+from ray_tracer_fragment_shader_amd.tracer import Tracer  # noqa: E402
+
+L = abi.lib()
+cfg = scenes.CONFIGS["c3"]
+W, H, B = cfg.width, cfg.height, cfg.depth
+cam = cfg.camera()
+
+
+def settle(fn, seconds):
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end:
+        for _ in range(16):
+            abi.check(fn(), "settle")
+        torch.cuda.synchronize()
+
+
+def wall_ms(fn, n, sync):
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        rc = fn()
+        if rc:
+            abi.check(rc, "timed")
+    sync()
+    return (time.perf_counter() - t0) * 1e3 / n
+
+
+def event_ms(fn, n, stream):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(n):
+        abi.check(fn(), "timed")
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+def part1(rounds):
+    null = torch.cuda.current_stream()
+    nb = torch.cuda.Stream()
+    t_multi, t_dev = Tracer(0), Tracer(0)
+    for t in (t_multi, t_dev):
+        t.set_scene(cfg.scene())
+    img = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+    g = ctypes.c_void_p()
+    arr = (ctypes.c_void_p * 1)(t_multi._ctx.value)
+    abi.check(L.rt_group_create(arr, 1, abi.RT_TRANSPORT_RCCL, ctypes.byref(g)), "rt_group_create")
+
+    def multi(st):
+        return lambda: L.rt_render_multi(g, ctypes.byref(cam), W, H, B, 0, abi.RT_OUT_RGBA8, None,
+                                         ctypes.c_void_p(img.data_ptr()), ctypes.c_void_p(st.cuda_stream))
+
+    def dev(st):
+        return lambda: L.rt_render_dev(t_dev._ctx, ctypes.byref(cam), W, H, B, None, None,
+                                       ctypes.c_void_p(img.data_ptr()), None, None, ctypes.c_void_p(st.cuda_stream))
+
+    def gsync():
+        abi.check(L.rt_group_synchronize(g), "rt_group_synchronize")
+        torch.cuda.synchronize()
+
+    modes = {"multi_null": multi(null), "multi_nonblocking": multi(nb), "dev_null": dev(null)}
+    res = {f"{m}_{k}": [] for m in modes for k in ("cold", "settled")}
+    idle, sett = float(os.environ.get("IDLE_S", "1.0")), float(os.environ.get("SETTLE_S", "0.25"))
+    for f in modes.values():
+        for _ in range(3):
+            abi.check(f(), "first renders")
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for m, f in modes.items():
+            time.sleep(idle)
+            for _ in range(20):
+                abi.check(f(), "warm")
+            res[f"{m}_cold"].append(wall_ms(f, 40, gsync))
+            settle(f, sett)
+            for _ in range(20):
+                abi.check(f(), "warm")
+            res[f"{m}_settled"].append(wall_ms(f, 40, gsync))
+    out = {k: round(statistics.median(v), 5) for k, v in res.items()}
+    out["dev_null_event_ms_serial"] = round(event_ms(modes["dev_null"], 40, null), 5)
+    print(json.dumps({"part": 1, "config": "c3", "idle_s": idle, "settle_s": sett, "rounds": rounds,
+                      "wall_ms_per_frame": out}), flush=True)
+    L.rt_group_destroy(g)
+    t_multi.close()
+    t_dev.close()
+
+
+def part2(ns):
+    t = Tracer(0)
+    t.set_scene(cfg.scene())
+    st = [torch.cuda.Stream(), torch.cuda.Stream()]
+    img = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+    # keep the GPU warm before the first measurement
+    full = lambda: L.rt_render_dev(t._ctx, ctypes.byref(cam), W, H, B, None, None, ctypes.c_void_p(img.data_ptr()),  # noqa
+                                   None, None, ctypes.c_void_p(st[0].cuda_stream))
+    settle(full, 0.3)
+    c3_serial = event_ms(full, 40, st[0])
+    for n in ns:
+        band, slab = ctypes.c_int(), ctypes.c_int()
+        abi.check(L.rt_band_plan(H, n, 0, ctypes.byref(band), ctypes.byref(slab)), "rt_band_plan")
+        hb, sr = band.value, slab.value
+        ranks = []
+        trs = [Tracer(0) for _ in range(n)]                 # one context per rank: its own view (rows) calibration
+        for r in range(n):
+            trs[r].set_scene(cfg.scene())
+            rows = abi.rt_rows(hb, n, r, 1)
+            slabs = [torch.empty((sr, W), dtype=torch.uint8, device="cuda") for _ in range(2)]
+
+            def one(b, rows=rows, slabs=slabs, tr=trs[r]):
+                return L.rt_render_dev_packed(tr._ctx, ctypes.byref(cam), W, H, B, ctypes.byref(rows), abi.RT_PIXEL_GRAY32F,
+                                              None, abi.RT_PIXEL_GRAY8, ctypes.c_void_p(slabs[b].data_ptr()),
+                                              ctypes.c_void_p(st[b].cuda_stream))
+            k = [0]
+
+            def alt(one=one, k=k):
+                k[0] += 1
+                return one(k[0] & 1)
+            for _ in range(3):                       # first render + calibration of this view (rows)
+                abi.check(one(0), "first")
+            torch.cuda.synchronize()
+            settle(full, 0.05)
+            ser = event_ms(lambda one=one: one(0), 40, st[0])
+            settle(full, 0.05)
+            two = wall_ms(alt, 80, torch.cuda.synchronize)
+            ranks.append({"rank": r, "serial_ms": round(ser, 5), "two_streams_ms": round(two, 5)})
+        gathered = torch.zeros((n * sr, W), dtype=torch.uint8, device="cuda")
+        up = lambda: L.rt_unpack_dev(ctypes.c_void_p(gathered.data_ptr()), ctypes.c_void_p(img.data_ptr()), W, H,  # noqa
+                                     abi.RT_PIXEL_GRAY8, abi.RT_PIXEL_RGBA8, hb, n, sr, ctypes.c_void_p(st[0].cuda_stream))
+        for _ in range(5):
+            abi.check(up(), "unpack")
+        unpack = event_ms(up, 40, st[0])
+        mser = max(x["serial_ms"] for x in ranks)
+        mtwo = max(x["two_streams_ms"] for x in ranks)
+        print(json.dumps({"part": 2, "n": n, "band_height": hb, "slab_rows": sr, "c3_serial_ms": round(c3_serial, 5),
+                          "ranks": ranks, "max_serial_ms": mser, "max_two_streams_ms": mtwo,
+                          "unpack_ms": round(unpack, 5),
+                          "bound_serial": round(c3_serial / (mser + unpack), 3),
+                          "bound_two_streams": round(c3_serial / (mtwo + unpack), 3)}), flush=True)
+        for x in trs:
+            x.close()
+    t.close()
+
+
+if __name__ == "__main__":
+    parts = os.environ.get("PARTS", "1,2").split(",")
+    if "1" in parts:
+        part1(int(os.environ.get("ROUNDS", "3")))
+    if "2" in parts:
+        part2([int(x) for x in os.environ.get("NS", "2,4,8").split(",")])
