@@ -308,6 +308,12 @@ def serial_kernel_ms(torch, L, abi, launch, stream, n=20):
 
 
 HBM_PEAK_GBS = 8000.0
+SETTLE_FRAMES_PER_S = 10000                            # c4 settle: frames per second of --settle (a c3 frame is ~0.11 ms)
+
+
+def settle_frames(settle_s):
+    """Untimed frames a group leg runs before timing: the same count on every rank (each frame is a collective)."""
+    return max(0, int(round(settle_s * SETTLE_FRAMES_PER_S)))
 
 
 def c4_scaling_keys(n, W, H, rays, c4_ms, c3_ms_inflight, c3_ms_serial):
@@ -329,6 +335,30 @@ def c4_scaling_keys(n, W, H, rays, c4_ms, c3_ms_inflight, c3_ms_serial):
     return out
 
 
+XGMI_LINK_GBS = 153.0                                   # nominal per-link rate (7 links per MI355X); not measured here
+
+
+def c4_projection_keys(n, c3_ms_per_frame, rank_ms, unpack_ms, slab_bytes):
+    """One GPU's projection of an n-rank c4 frame (rt_render_multi at n ranks cannot run on one GPU): every rank's band
+    set rendered alone the way the group renders it (rank_ms[r], per frame, frames in flight as the group keeps them),
+    and rank 0's unpack of the n-rank gathered buffer.  Rank 0 renders its bands and unpacks on one GPU, so the
+    projected frame interval is max(rank_ms) + unpack_ms (the unpack counted in full, although it runs on rank 0's
+    high-priority stream beside the next render); the gather itself (each peer's slab_bytes over its own xGMI link into
+    rank 0, double-buffered behind the next render) is reported at the nominal link rate, not measured, and bounds the
+    interval only if it is the longest stage."""
+    render = max(rank_ms)
+    frame = render + unpack_ms
+    xfer = slab_bytes / (XGMI_LINK_GBS * 1e9) * 1e3
+    bound = max(frame, xfer)
+    key = f"n{n}"
+    return {f"{key}_rank_render_ms": [round(x, 5) for x in rank_ms], f"{key}_rank_render_ms_max": round(render, 5),
+            f"{key}_unpack_ms": round(unpack_ms, 5), f"{key}_projected_frame_ms": round(bound, 5),
+            f"{key}_gather_ms_nominal": round(xfer, 5),
+            f"{key}_limiting_stage": ("gather (nominal xGMI)" if xfer > frame else
+                                      "rank render" if render >= unpack_ms else "unpack"),
+            f"{key}_speedup_bound": round(c3_ms_per_frame / bound, 3)}
+
+
 def c4_parallelism_text(n, c4):
     """The top-level `parallelism` suffix that carries the row-split c4 curve at N > 1 (SCALE records)."""
     if not c4 or "speedup_vs_c3_1gpu" not in c4:
@@ -338,10 +368,11 @@ def c4_parallelism_text(n, c4):
             f"(efficiency {c4['efficiency']}), HBM-write {c4['hbm_write_frac_per_gpu']} of peak per GPU")
 
 
-def c3_one_gpu(torch, L, abi, Tracer, cfg, dev, local, nfly, steps):
+def c3_one_gpu(torch, L, abi, Tracer, cfg, dev, local, nfly, steps, settle_s):
     """One GPU's c3 frame as the c4 leg's denominator: RGBA8 only (the group leg's output), calibrated view, `nfly`
-    frames in flight on their own streams (the bench's timed pattern) and one stream serial.  -> (ms in flight, ms
-    serial)."""
+    frames in flight on their own streams (the bench's timed pattern) and one stream serial, after `settle_s` seconds of
+    untimed frames (the GPU's clocks ramp up under load: a leg timed right after an idle stretch measured 14% slower,
+    tools/c4_gap_probe.py).  -> (ms in flight, ms serial)."""
     W, H, B = cfg.width, cfg.height, cfg.depth
     cam = cfg.camera()
     ts = [Tracer(local) for _ in range(nfly)]
@@ -355,11 +386,62 @@ def c3_one_gpu(torch, L, abi, Tracer, cfg, dev, local, nfly, steps):
         for a in la:
             abi.check(L.rt_render_dev(*a), "rt_render_dev")
     torch.cuda.synchronize()
-    _, ms_fly = pipelined_frames(torch, L, abi, ts, ss, la, steps, 0.0)
+    _, ms_fly = pipelined_frames(torch, L, abi, ts, ss, la, steps, settle_s)
     ms_ser = serial_kernel_ms(torch, L, abi, la[0], ss[0], n=steps)
     for t in ts:
         t.close()
     return ms_fly, ms_ser
+
+
+def c4_rank_projection(torch, L, abi, Tracer, cfg, dev, local, n, band_height, c3_ms_per_frame, frames=120):
+    """One GPU's projection of the c4 frame at n ranks (c4_projection_keys): each rank r's band set (rt_rows(hb, n, r),
+    the band plan rt_render_multi uses) rendered alone as the group renders it — GRAY8 wire format into a slab, the
+    rank's two render streams taking frames in turn, one context per rank — timed over `frames` frames after the
+    calibration renders; then rank 0's rt_unpack_dev of an n-rank gathered GRAY8 buffer into the RGBA8 image."""
+    W, H, B = cfg.width, cfg.height, cfg.depth
+    cam = cfg.camera()
+    band, slab = ctypes.c_int(), ctypes.c_int()
+    abi.check(L.rt_band_plan(H, n, band_height, ctypes.byref(band), ctypes.byref(slab)), "rt_band_plan")
+    hb, sr = band.value, slab.value
+    sts = [torch.cuda.Stream(dev) for _ in range(2)]
+    rank_ms = []
+    for r in range(n):
+        t = Tracer(local)
+        t.set_scene(cfg.scene())
+        rows = abi.rt_rows(hb, n, r, 1)
+        slabs = [torch.empty((sr, W), dtype=torch.uint8, device=dev) for _ in range(2)]
+        la = [(t._ctx, ctypes.byref(cam), W, H, B, ctypes.byref(rows), abi.RT_PIXEL_GRAY32F, None, abi.RT_PIXEL_GRAY8,
+               ctypes.c_void_p(slabs[k].data_ptr()), ctypes.c_void_p(sts[k].cuda_stream)) for k in range(2)]
+        for _ in range(3):                                   # first render and calibration of the rank's view
+            abi.check(L.rt_render_dev_packed(*la[0]), "rt_render_dev_packed")
+        abi.check(L.rt_render_dev_packed(*la[1]), "rt_render_dev_packed")
+        for f in range(frames // 2):                          # warm (untimed)
+            abi.check(L.rt_render_dev_packed(*la[f & 1]), "rt_render_dev_packed")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for f in range(frames):
+            rc = L.rt_render_dev_packed(*la[f & 1])
+            if rc:
+                abi.check(rc, "rt_render_dev_packed")
+        torch.cuda.synchronize()
+        rank_ms.append((time.perf_counter() - t0) * 1e3 / frames)
+        t.close()
+    gathered = torch.zeros((n * sr, W), dtype=torch.uint8, device=dev)
+    img = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
+    ua = (ctypes.c_void_p(gathered.data_ptr()), ctypes.c_void_p(img.data_ptr()), W, H, abi.RT_PIXEL_GRAY8,
+          abi.RT_PIXEL_RGBA8, hb, n, sr, ctypes.c_void_p(sts[0].cuda_stream))
+    for _ in range(10):
+        abi.check(L.rt_unpack_dev(*ua), "rt_unpack_dev")
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    torch.cuda.synchronize()
+    e[0].record(sts[0])
+    for _ in range(40):
+        abi.check(L.rt_unpack_dev(*ua), "rt_unpack_dev")
+    e[1].record(sts[0])
+    torch.cuda.synchronize()
+    keys = c4_projection_keys(n, c3_ms_per_frame, rank_ms, e[0].elapsed_time(e[1]) / 40, sr * W)
+    keys[f"n{n}_band_height"] = hb
+    return keys
 
 
 def packed_host_legs(t, sa, cam, W, H, B, k=30):
@@ -568,7 +650,11 @@ def main() -> int:
             dist.init_process_group("gloo")
     L = abi.lib()
     dev = torch.device("cuda", local)
-    stream = torch.cuda.current_stream(dev)
+    # Every leg runs on ordinary (non-null) streams: the legacy null stream's implicit ordering cost the c2 frames in
+    # flight 26.4 us per frame against 23.8 on three pool streams, and 0.7 us per serial launch (tools/c4_gap_probe.py
+    # part 3, BENCH_r05).  This process's current stream becomes one, so torch work stays ordered with it.
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
 
     def barrier():
         if world > 1:
@@ -636,7 +722,10 @@ def main() -> int:
             abi.check(L.rt_group_synchronize(g), "rt_group_synchronize")
             torch.cuda.synchronize()
 
-        for _ in range(max(warmup, 20)):                  # includes the tile-order calibration of every rank
+        # untimed: the tile-order calibration of every rank, then frames until the clocks have ramped up — a fixed
+        # count on every rank (each frame is a collective), SETTLE_FRAMES_PER_S per second of --settle (BENCH_r05's
+        # one-rank frame, timed after the 20 warm-up frames alone, was 14% slower than settled: tools/c4_gap_probe.py)
+        for _ in range(max(warmup, 20) + settle_frames(args.settle)):
             abi.check(fn(*argv), "rt_render_multi")
         sync()
         if not copy_ranks:
@@ -765,7 +854,7 @@ def main() -> int:
             trs = [tr] + [Tracer(local) for _ in range(nfly - 1)]
             for t in trs[1:]:
                 t.set_scene(scene)
-            sts = [stream] + [torch.cuda.Stream(dev) for _ in range(nfly - 1)]
+            sts = [stream] + [torch.cuda.Stream(dev) for _ in range(nfly - 1)]         # (pool streams, not null)
             outs = [(torch.empty((nl, W, 4), dtype=torch.float32, device=dev),
                      torch.empty((nl, W, 4), dtype=torch.uint8, device=dev)) for _ in range(nfly)]
             launch_args = [(trs[i]._ctx, ctypes.byref(cam), W, H, B, None, ctypes.c_void_p(outs[i][0].data_ptr()),
@@ -930,8 +1019,8 @@ def main() -> int:
             steps4 = 40                                    # (fixed: the first launch and the final sync weigh less)
             # the denominator of the split frame's speed-up: the same job's one-GPU c3 frame (same scene, view and
             # RGBA8 output), measured on rank 0 before the group leg at every N
-            base = (c3_one_gpu(torch, L, abi, Tracer, c3, dev, local, max(1, args.frames_in_flight), steps4)
-                    if rank == 0 else None)
+            base = (c3_one_gpu(torch, L, abi, Tracer, c3, dev, local, max(1, args.frames_in_flight), steps4,
+                               args.settle) if rank == 0 else None)
             barrier()
             if rehearsal:                                   # gloo on one GPU: rank 0 drives `world` COPY ranks
                 info, el4 = group_leg(c3, steps4, 3, copy_ranks=world) if rank == 0 else ({}, 0.0)
@@ -951,6 +1040,18 @@ def main() -> int:
             if rank == 0 and base and "error" not in info:
                 info.update(c4_scaling_keys(info["ranks"], c3.width, c3.height, info["rays_per_frame"],
                                             el4 / steps4 * 1e3, *base))
+                if world == 1:                              # what one GPU says about 2, 4 and 8 ranks
+                    proj = {}
+                    for n in (2, 4, 8):
+                        proj.update(c4_rank_projection(torch, L, abi, Tracer, c3, dev, local, n, args.band_height,
+                                                       base[0]))
+                    proj["note"] = ("one-GPU projection of the c4 frame at n ranks (rt_render_multi at n > 1 needs n "
+                                    "GPUs): nN_rank_render_ms = each rank's band set rendered alone as the group "
+                                    "renders it (GRAY8 slab, two render streams taking frames in turn), "
+                                    "nN_projected_frame_ms = the slowest rank + rank 0's unpack of the gathered GRAY8 "
+                                    "buffer (or the nominal xGMI gather of one slab if longer), nN_speedup_bound = "
+                                    "c3_1gpu_ms_per_frame / nN_projected_frame_ms")
+                    info["projection"] = proj
                 info["scaling_note"] = ("speedup_vs_c3_1gpu = c3_1gpu_ms_per_frame (one GPU, RGBA8 only, "
                                         f"{max(1, args.frames_in_flight)} frames in flight, measured on rank 0 of this "
                                         "job before the group leg) / ms_per_frame; efficiency = speedup / ranks; "

@@ -7,7 +7,8 @@
 // imbalanced: sky rows are cheap, board rows are not), rank r rendering bands b = r (mod n) densely into its
 // slab (rt_rows).  The only data-path exchange is the gather of the slabs to rank 0:
 //
-//   render stream rs_r:  wait sent[r][b] -> rt_render_dev(rows of r) into slab[r][b] -> record rendered[r][b]
+//   render stream rs_r[k] (k alternates per frame of a static view: consecutive frames' renders overlap):
+//                        wait sent[r][b] -> rt_render_dev(rows of r) into slab[r][b] -> record rendered[r][b]
 //   comm stream   cs_r:  wait rendered[r][b] -> ncclSend(slab[r][b] -> rank 0)      -> record sent[r][b]
 //   root cs_0:           ncclRecv(gathered[b] + q*slab <- q), q = 1..n-1 (posted at once: they do not wait for
 //                        the root's own render); wait the caller stream's earlier work (received[b]) and the
@@ -15,7 +16,7 @@
 //                        -> record assembled[b]; the caller's stream waits for assembled[b]
 // A process's ranks must switch scenes between the same frames: one-process-per-GPU groups agree on the scene
 // (hence the wire formats) with a small all-reduce whenever a rank's scene changes (agree_on_scene).
-// Stream priorities: rs lowest, cs highest (the gather's kernels do not queue behind the next render grid).
+// Stream priorities: rs[0], rs[1] lowest, cs highest (the gather's kernels do not queue behind the next render grid).
 // A one-rank group renders straight into the caller's image on the caller's stream (identity band plan).
 //
 // What travels: the wire formats.  An achromatic scene (every colour term with R = G = B, rt_scene_achromatic)
@@ -58,7 +59,13 @@ struct Rank {
     rt_ctx* ctx = nullptr;
     int device = 0;
     int rank = 0;
-    hipStream_t rs = nullptr, cs = nullptr;    // render / comm streams (on `device`)
+    // Two render streams and a comm stream (on `device`).  A frame renders on rs[k]: a static view alternates k, so a
+    // frame's bands start while the previous frame's last waves drain (a 1/8 band set of the c4 frame is a short
+    // launch whose tail is one long wave: 27 us serial, 15 us per frame on two streams, tools/c4_gap_probe.py part 3);
+    // a new camera stays on the previous frame's stream (its per-eye preparation rewrites state the other stream's
+    // render may still read, which the context would otherwise resolve with a device synchronisation).
+    hipStream_t rs[2] = {nullptr, nullptr}, cs = nullptr;
+    int last_rs = 1;                           // rs index of the previous frame
     hipEvent_t rendered[2] = {nullptr, nullptr};
     hipEvent_t sent[2] = {nullptr, nullptr};   // on cs (RCCL) or on the root's comm stream (COPY)
     bool sent_rec[2] = {false, false};
@@ -99,6 +106,10 @@ struct rt_group {
     rt_group_plan root_plan{};
     int plan_key[5] = {0, 0, 0, 0, 0};
     bool plan_valid = false;
+    // the previous frame's camera (a static view alternates the ranks' render streams, Rank::rs)
+    rt_camera last_cam{};
+    bool last_cam_valid = false;
+    int render_streams = 2;                    // RT_GROUP_RENDER_STREAMS (A/B): 1 renders every frame on rs[0]
 };
 
 namespace {
@@ -135,7 +146,7 @@ int setup_rank(Rank* r, rt_ctx* ctx, int rank, hipEvent_t* sent_device_events) {
     // queueing behind the next frame's render grid, so the exchange overlaps the render.
     int least = 0, greatest = 0;
     G_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    G_HIP(hipStreamCreateWithPriority(&r->rs, hipStreamNonBlocking, least));
+    for (int k = 0; k < 2; ++k) G_HIP(hipStreamCreateWithPriority(&r->rs[k], hipStreamNonBlocking, least));
     G_HIP(hipStreamCreateWithPriority(&r->cs, hipStreamNonBlocking, greatest));
     for (int b = 0; b < 2; ++b) {
         G_HIP(hipEventCreateWithFlags(&r->rendered[b], hipEventDisableTiming));
@@ -169,7 +180,8 @@ extern "C" int rt_group_destroy(rt_group* g) {
     if (!g) return RT_OK;
     for (auto& r : g->ranks) {
         (void)hipSetDevice(r.device);
-        if (r.rs) (void)hipStreamSynchronize(r.rs);
+        for (hipStream_t s : r.rs)
+            if (s) (void)hipStreamSynchronize(s);
         if (r.cs) (void)hipStreamSynchronize(r.cs);
     }
     for (auto& r : g->ranks) {
@@ -185,7 +197,8 @@ extern "C" int rt_group_destroy(rt_group* g) {
             for (int k = 0; k < kKinds; ++k)
                 if (r.slab[b][k]) (void)hipFree(r.slab[b][k]);
         }
-        if (r.rs) (void)hipStreamDestroy(r.rs);
+        for (hipStream_t s : r.rs)
+            if (s) (void)hipStreamDestroy(s);
         if (r.cs) (void)hipStreamDestroy(r.cs);
     }
     if (g->owns_root && !g->ranks.empty()) {
@@ -226,6 +239,7 @@ extern "C" int rt_group_create(rt_ctx* const* ctxs, int n, int transport, rt_gro
         return rt_fail(RT_EINVAL, "rt_group_create: RCCL needs one context per device (use RT_TRANSPORT_COPY)");
     rt_group* g = new rt_group();
     if (const char* e = getenv("RT_GATHER_ROOT_WAITS")) g->root_waits = atoi(e) != 0;
+    if (const char* e = getenv("RT_GROUP_RENDER_STREAMS")) g->render_streams = atoi(e) == 1 ? 1 : 2;
     g->n_ranks = n;
     g->transport = transport;
     g->owns_root = true;
@@ -268,6 +282,7 @@ extern "C" int rt_group_create_rank(rt_ctx* ctx, int n_ranks, int rank, const ui
         return rt_fail(RT_EINVAL, "rt_group_create_rank: bad arguments");
     rt_group* g = new rt_group();
     if (const char* e = getenv("RT_GATHER_ROOT_WAITS")) g->root_waits = atoi(e) != 0;
+    if (const char* e = getenv("RT_GROUP_RENDER_STREAMS")) g->render_streams = atoi(e) == 1 ? 1 : 2;
     g->n_ranks = n_ranks;
     g->transport = RT_TRANSPORT_RCCL;
     g->owns_root = rank == 0;
@@ -303,7 +318,7 @@ extern "C" int rt_group_synchronize(rt_group* g) {
     if (!g) return rt_fail(RT_EINVAL, "rt_group_synchronize: null group");
     for (auto& r : g->ranks) {
         G_HIP(hipSetDevice(r.device));
-        G_HIP(hipStreamSynchronize(r.rs));
+        for (hipStream_t s : r.rs) G_HIP(hipStreamSynchronize(s));
         G_HIP(hipStreamSynchronize(r.cs));
     }
     return RT_OK;
@@ -526,21 +541,28 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
             if ((rc = phase_events(g->ranks[q], slot, q == 0 && g->owns_root, &pe[q]))) return rc;
 
     // ---- render: every local rank's bands into slab[b], in the wire formats ---------------------------------
+    // (rs[k]: the other render stream than the previous frame's for an unchanged camera; RT_GROUP_RENDER_STREAMS=1: one)
+    const bool same_view = g->last_cam_valid && memcmp(&g->last_cam, cam, sizeof(rt_camera)) == 0;
     for (size_t q = 0; q < g->ranks.size(); ++q) {
         Rank& r = g->ranks[q];
+        const int k = g->render_streams > 1 && same_view ? 1 - r.last_rs : r.last_rs;
+        const hipStream_t rs = r.rs[k];
+        r.last_rs = k;
         G_HIP(hipSetDevice(r.device));
-        if (r.sent_rec[b]) G_HIP(hipStreamWaitEvent(r.rs, r.sent[b], 0));     // slab[b] has left (frame - 2)
+        if (r.sent_rec[b]) G_HIP(hipStreamWaitEvent(rs, r.sent[b], 0));       // slab[b] has left (frame - 2)
         if (r.rank == 0 && g->assembled_rec[b])                               // the root's slab[b] is read by
-            G_HIP(hipStreamWaitEvent(r.rs, g->assembled[b], 0));              // frame - 2's unshuffle
-        if (pe[q]) G_HIP(hipEventRecord(pe[q]->r0, r.rs));
+            G_HIP(hipStreamWaitEvent(rs, g->assembled[b], 0));                // frame - 2's unshuffle
+        if (pe[q]) G_HIP(hipEventRecord(pe[q]->r0, rs));
         rt_rows rows = {hb, g->n_ranks, r.rank, 1};
         rc = rt_render_dev_packed(r.ctx, cam, W, H, depth, &rows, wire[0], kind_on[0] ? r.slab[b][0] : nullptr,
-                                  wire[1], kind_on[1] ? r.slab[b][1] : nullptr, r.rs);
+                                  wire[1], kind_on[1] ? r.slab[b][1] : nullptr, rs);
         if (rc) return rc;
         G_HIP(hipSetDevice(r.device));
-        if (pe[q]) G_HIP(hipEventRecord(pe[q]->r1, r.rs));
-        G_HIP(hipEventRecord(r.rendered[b], r.rs));
+        if (pe[q]) G_HIP(hipEventRecord(pe[q]->r1, rs));
+        G_HIP(hipEventRecord(r.rendered[b], rs));
     }
+    g->last_cam = *cam;
+    g->last_cam_valid = true;
 
     // ---- gather to rank 0 ------------------------------------------------------------------------------------
     // rank 0's receive from peer q for image k: offset into gathered[b][k] and bytes (= q's send_bytes[k])

@@ -250,11 +250,12 @@ extern "C" int rt_band_plan(int height, int n_ranks, int band_height, int* band_
         return rt_fail(RT_EINVAL, "rt_band_plan: bad arguments");
     int hb = band_height;
     if (hb == 0) {
-        // Largest band height <= 16 giving every rank the same rows (e.g. 15 for 1080 rows over 8 ranks);
-        // 8 when no such height exists (ranks then differ by at most one band).
+        // The render's tile height (8 rows): every 8 x 8 tile of a rank's slab is then 8 consecutive image rows, which
+        // the per-wave primary cone culling needs (a tile straddling two bands tests every sphere).  Ranks differ by
+        // at most one band (c4 at 8 ranks: 272 against 264 rows).  r02-r05 chose the largest height <= 16 giving
+        // every rank the same rows (15 for 2160 rows over 8 ranks): its straddling tiles made every rank's band set
+        // 10% slower (tools/c4_gap_probe.py part 2: 30.4 -> 27.5 us per 1/8 frame serial).
         hb = 8;
-        for (int h = 16; h >= 1; --h)
-            if (height % (h * n_ranks) == 0) { hb = h; break; }
     }
     if (n_ranks == 1) hb = std::max(hb, 1);
     int slab = 0;

@@ -278,9 +278,28 @@ __global__ __launch_bounds__(kThreads) void rt_unshuffle_kernel(const uint32_t* 
 //   kUnpackGray8: GRAY8 -> RGBA8 (g, g, g, 255);  kUnpackRgb8: RGB8 -> RGBA8 (r, g, b, 255);
 //   kUnpackGray32f: GRAY32F -> RGBA32F (v, v, v, 1).
 // Exact: the render kernel writes these very bytes into the RGBA images (achromatic scenes: R = G = B bit for
-// bit).  VEC: W % 4 == 0 and 16-byte aligned buffers — 4 pixels per work-item step, 16-byte stores.
+// bit).  VEC (16-byte aligned buffers, W % 4 == 0): 4 — 4 pixels per work-item step, 16-byte stores; 16 — a byte
+// wire format: the same 16-byte stores, four steps per lane unrolled with their loads issued first, so a
+// 4K row is one round trip per lane instead of four dependent ones (DESIGN §7 has the times).
 constexpr int kUnpackGray8 = 0, kUnpackRgb8 = 1, kUnpackGray32f = 2;
-template <int MODE, bool VEC>
+__device__ __forceinline__ uint4 gray4_rgba(uint32_t g) {
+    uint4 o;
+    o.x = (g & 0xffu) * 0x010101u | 0xff000000u;
+    o.y = ((g >> 8) & 0xffu) * 0x010101u | 0xff000000u;
+    o.z = ((g >> 16) & 0xffu) * 0x010101u | 0xff000000u;
+    o.w = (g >> 24) * 0x010101u | 0xff000000u;
+    return o;
+}
+// three little-endian words r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3 -> four RGBA8 pixels
+__device__ __forceinline__ uint4 rgb4_rgba(uint32_t a, uint32_t b, uint32_t c) {
+    uint4 o;
+    o.x = (a & 0xffffffu) | 0xff000000u;
+    o.y = (a >> 24) | ((b & 0xffffu) << 8) | 0xff000000u;
+    o.z = (b >> 16) | ((c & 0xffu) << 16) | 0xff000000u;
+    o.w = (c >> 8) | 0xff000000u;
+    return o;
+}
+template <int MODE, int VEC>
 __global__ __launch_bounds__(kThreads) void rt_unpack_kernel(const uint8_t* __restrict__ src,
                                                              const uint8_t* __restrict__ src0,
                                                              uint8_t* __restrict__ dst, int W, int height,
@@ -291,26 +310,43 @@ __global__ __launch_bounds__(kThreads) void rt_unpack_kernel(const uint8_t* __re
     constexpr size_t out_px = MODE == kUnpackGray32f ? 16 : 4;
     const uint8_t* s = gathered_row(src, src0, j, band_height, n_ranks, slab_rows, (size_t)W * in_px);
     uint8_t* d = dst + (size_t)j * W * out_px;
+    if (VEC == 16 && MODE != kUnpackGray32f) {
+        // four 4-pixel quads per lane, kThreads apart (every load and store instruction covers a contiguous run of the
+        // row), the four loads issued before the first store
+        const int groups = W >> 2;
+        uint4* d4 = reinterpret_cast<uint4*>(d);
+        for (int q0 = threadIdx.x; q0 < groups; q0 += 4 * kThreads) {
+            uint32_t a[4], b[4], c[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = q0 + u * kThreads;
+                if (q < groups) {
+                    if (MODE == kUnpackGray8) {
+                        a[u] = reinterpret_cast<const uint32_t*>(s)[q];
+                    } else {
+                        const uint32_t* s3 = reinterpret_cast<const uint32_t*>(s) + 3 * q;
+                        a[u] = s3[0];
+                        b[u] = s3[1];
+                        c[u] = s3[2];
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = q0 + u * kThreads;
+                if (q < groups) d4[q] = MODE == kUnpackGray8 ? gray4_rgba(a[u]) : rgb4_rgba(a[u], b[u], c[u]);
+            }
+        }
+        return;
+    }
     if (VEC) {
         const int groups = W >> 2;
         for (int q = threadIdx.x; q < groups; q += kThreads) {
             if (MODE == kUnpackGray8) {
-                const uint32_t g = reinterpret_cast<const uint32_t*>(s)[q];
-                uint4 o;
-                o.x = (g & 0xffu) * 0x010101u | 0xff000000u;
-                o.y = ((g >> 8) & 0xffu) * 0x010101u | 0xff000000u;
-                o.z = ((g >> 16) & 0xffu) * 0x010101u | 0xff000000u;
-                o.w = (g >> 24) * 0x010101u | 0xff000000u;
-                reinterpret_cast<uint4*>(d)[q] = o;
+                reinterpret_cast<uint4*>(d)[q] = gray4_rgba(reinterpret_cast<const uint32_t*>(s)[q]);
             } else if (MODE == kUnpackRgb8) {
                 const uint32_t* s3 = reinterpret_cast<const uint32_t*>(s) + 3 * q;
-                const uint32_t a = s3[0], b = s3[1], c = s3[2];      // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
-                uint4 o;
-                o.x = (a & 0xffffffu) | 0xff000000u;
-                o.y = (a >> 24) | ((b & 0xffffu) << 8) | 0xff000000u;
-                o.z = (b >> 16) | ((c & 0xffu) << 16) | 0xff000000u;
-                o.w = (c >> 8) | 0xff000000u;
-                reinterpret_cast<uint4*>(d)[q] = o;
+                reinterpret_cast<uint4*>(d)[q] = rgb4_rgba(s3[0], s3[1], s3[2]);
             } else {
                 const float4 v = reinterpret_cast<const float4*>(s)[q];
                 float4* o = reinterpret_cast<float4*>(d) + 4 * q;
@@ -1562,6 +1598,12 @@ extern "C" int rt_unshuffle_dev(const void* gathered, void* image, int W, int H,
     return rt_unshuffle_dev_ex(gathered, nullptr, image, W, H, elem_bytes, band_height, n_ranks, slab_rows, stream);
 }
 
+// RT_UNPACK_VEC4=1 (A/B): the 4-pixel steps for byte formats too (r05's kernel)
+static const bool g_unpack_vec4 = [] {
+    const char* e = getenv("RT_UNPACK_VEC4");
+    return e && atoi(e) != 0;
+}();
+
 int rt_unpack_dev_ex(const void* gathered, const void* rank0_slab, void* image, int W, int H, int src_format,
                      int dst_format, int band_height, int n_ranks, int slab_rows, void* stream) {
     int sb = 0, db = 0;
@@ -1577,7 +1619,8 @@ int rt_unpack_dev_ex(const void* gathered, const void* rank0_slab, void* image, 
     else if (src_format == RT_PIXEL_RGB8 && dst_format == RT_PIXEL_RGBA8) mode = kUnpackRgb8;
     else if (src_format == RT_PIXEL_GRAY32F && dst_format == RT_PIXEL_RGBA32F) mode = kUnpackGray32f;
     else return rt_fail(RT_EINVAL, "rt_unpack_dev: unsupported format pair");
-    const bool vec = W % 4 == 0 && ((uintptr_t)gathered | (uintptr_t)rank0_slab | (uintptr_t)image) % 16 == 0;
+    const bool al16 = ((uintptr_t)gathered | (uintptr_t)rank0_slab | (uintptr_t)image) % 16 == 0;
+    const int vec = !al16 || W % 4 != 0 ? 0 : mode != kUnpackGray32f && !g_unpack_vec4 ? 16 : 4;
     const uint8_t* g = (const uint8_t*)gathered;
     const uint8_t* g0 = (const uint8_t*)rank0_slab;
     uint8_t* im = (uint8_t*)image;
@@ -1585,9 +1628,13 @@ int rt_unpack_dev_ex(const void* gathered, const void* rank0_slab, void* image, 
     const dim3 grid((unsigned)H), blk(kThreads);
 #define RT_UNPACK(M, V) hipLaunchKernelGGL((rt_unpack_kernel<M, V>), grid, blk, 0, st, g, g0, im, W, H, band_height, \
                                            n_ranks, slab_rows)
-    if (mode == kUnpackGray8) { if (vec) RT_UNPACK(kUnpackGray8, true); else RT_UNPACK(kUnpackGray8, false); }
-    else if (mode == kUnpackRgb8) { if (vec) RT_UNPACK(kUnpackRgb8, true); else RT_UNPACK(kUnpackRgb8, false); }
-    else { if (vec) RT_UNPACK(kUnpackGray32f, true); else RT_UNPACK(kUnpackGray32f, false); }
+    if (mode == kUnpackGray8) {
+        if (vec == 16) RT_UNPACK(kUnpackGray8, 16); else if (vec) RT_UNPACK(kUnpackGray8, 4); else RT_UNPACK(kUnpackGray8, 0);
+    } else if (mode == kUnpackRgb8) {
+        if (vec == 16) RT_UNPACK(kUnpackRgb8, 16); else if (vec) RT_UNPACK(kUnpackRgb8, 4); else RT_UNPACK(kUnpackRgb8, 0);
+    } else {
+        if (vec) RT_UNPACK(kUnpackGray32f, 4); else RT_UNPACK(kUnpackGray32f, 0);
+    }
 #undef RT_UNPACK
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_unpack_kernel: ") + hipGetErrorString(e));

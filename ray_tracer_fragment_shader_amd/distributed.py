@@ -24,9 +24,13 @@ import torch.distributed as dist
 from . import abi, scenes
 
 
-def auto_band_height(height: int, world: int, preferred: int = 8) -> int:
-    """Largest band height <= 16 that gives every rank the same number of rows per frame (falls back to
-    `preferred`): e.g. 15 rows for 1080 rows over 8 ranks."""
+def auto_band_height(height: int, world: int, preferred: int = 8, equal_rows: bool = False) -> int:
+    """The render's tile height, 8 rows (rt_band_plan's choice: tile-aligned bands keep the per-wave cone culling;
+    ranks differ by at most one band); with `equal_rows` (frame streams: the all-to-all needs every rank's rows equal)
+    the largest band height <= 16 that gives every rank the same number of rows per frame, falling back to
+    `preferred` (e.g. 15 rows for 1080 rows over 8 ranks)."""
+    if not equal_rows:
+        return 8
     for hb in range(16, 0, -1):
         if height % (hb * world) == 0:
             return hb
@@ -34,13 +38,16 @@ def auto_band_height(height: int, world: int, preferred: int = 8) -> int:
 
 
 class BandPlan:
-    """Row-band partition of `frames` stacked height-row frames over `world` ranks."""
+    """Row-band partition of `frames` stacked height-row frames over `world` ranks.  equal_rows (default: frames > 1,
+    the frame streams' all-to-all) asks the automatic band height for the same rows on every rank."""
 
-    def __init__(self, height: int, world: int, band_height: Optional[int] = None, frames: int = 1):
+    def __init__(self, height: int, world: int, band_height: Optional[int] = None, frames: int = 1,
+                 equal_rows: Optional[bool] = None):
         self.height = height
         self.world = world
         self.frames = frames
-        self.band_height = band_height or auto_band_height(height, world)
+        eq = frames > 1 if equal_rows is None else equal_rows
+        self.band_height = band_height or auto_band_height(height, world, equal_rows=eq)
         self.frame_local = [scenes.local_rows(height, self.rows(r, 1)) for r in range(world)]
         self.local = [n * frames for n in self.frame_local]
         self.slab_rows = max(self.frame_local) if world > 0 else 0     # rows per frame, padded

@@ -176,8 +176,12 @@ def test_band_plan_matches_host_plan(H, n, hb):
     assert band.value == plan.band_height
     assert slab.value == plan.slab_rows
     assert sum(plan.frame_local) == H
-    if H == 2160 and n == 8:
-        assert band.value == 15 and plan.balanced
+    assert max(plan.frame_local) - min(plan.frame_local) <= plan.band_height
+    if hb == 0:                                  # tile-aligned bands (8 x 8 tiles never straddle two bands)
+        assert band.value == 8
+    if H == 2160 and n == 8:                     # the frame streams' equal-rows plan
+        eq = BandPlan(H, n, None, equal_rows=True)
+        assert eq.band_height == 15 and eq.balanced
     assert L.rt_band_plan(H, 0, 0, ctypes.byref(band), None) == abi.RT_EINVAL
 
 

@@ -128,3 +128,17 @@ def test_cpu_baseline_labels_threads_not_cores():
     assert "not physical cores" in lab["threads_note"] and "OMP_NUM_THREADS=16" in lab["threads_note"]
     assert lab["nproc"] == os.cpu_count() and lab["affinity_threads"] >= 1
     assert lab["omp_num_threads_env"] == "16" and "host_cpu" in lab and lab["unit"] == "Mray/s"
+
+
+def test_c4_projection_keys():
+    """The one-GPU projection of the 8-rank c4 frame: slowest rank's band render + rank 0's unpack, or the nominal
+    gather when that is longer; speed-up bound against the one-GPU c3 frame."""
+    k = bench.c4_projection_keys(8, 0.112, [0.015, 0.0165, 0.016], 0.003, 1_044_480)
+    assert k["n8_rank_render_ms_max"] == 0.0165 and k["n8_unpack_ms"] == 0.003
+    assert k["n8_projected_frame_ms"] == round(0.0165 + 0.003, 5)
+    assert k["n8_speedup_bound"] == round(0.112 / 0.0195, 3)
+    assert k["n8_limiting_stage"] == "rank render"
+    assert abs(k["n8_gather_ms_nominal"] - 1_044_480 / 153e9 * 1e3) < 1e-5
+    slow = bench.c4_projection_keys(8, 0.112, [0.001], 0.0005, 10_000_000)      # gather-bound
+    assert slow["n8_limiting_stage"] == "gather (nominal xGMI)"
+    assert slow["n8_projected_frame_ms"] == slow["n8_gather_ms_nominal"]

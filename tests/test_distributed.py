@@ -118,7 +118,8 @@ def test_auto_band_height_balances_bench_sizes():
             p = BandPlan(H, N, frames=N)
             assert p.balanced, (H, N, p.band_height)
             assert sum(p.frame_local) == H and p.local[0] == N * p.frame_local[0]
-    assert 1080 % (auto_band_height(1080, 8) * 8) == 0
+    assert 1080 % (auto_band_height(1080, 8, equal_rows=True) * 8) == 0
+    assert auto_band_height(1080, 8) == 8                     # single frames: the tile height
 
 
 # ---- the product's group protocol (rt_group_plan.cpp), driven from real processes without a GPU -------------------

@@ -87,7 +87,8 @@ def test_chromatic_scene_rejects_gray_and_packs_rgb(tr):
         tr.render_packed(cam, W, H, 5, P.RT_PIXEL_RGB8, None)
 
 
-@pytest.mark.parametrize("W", [480, 477])                       # W % 4: vector and per-pixel unpack paths
+# W % 4 == 0: unrolled 4-pixel steps (4352: more than one unrolled step per lane), else per pixel
+@pytest.mark.parametrize("W", [480, 4352, 484, 477])
 @pytest.mark.parametrize("G,hb", [(1, 0), (3, 5), (8, 0)])
 def test_unpack_dev_expands_bands(tr, W, G, hb):
     """rt_unpack_dev: G ranks' packed bands -> RGBA images in image order, equal to the one-launch images."""

@@ -111,59 +111,160 @@ def part1(rounds):
 
 
 def part2(ns):
+    """Per rank r of n: its band set rendered alone as GRAY8, serial (one stream) and with K streams taking frames in
+    turn (K = 2, 3: frames of the same rank overlapping, the group's double / triple buffering), for each band height
+    in HBS (0: rt_band_plan's choice); rank 0's rt_unpack_dev of an n-rank gathered GRAY8 buffer."""
     t = Tracer(0)
     t.set_scene(cfg.scene())
-    st = [torch.cuda.Stream(), torch.cuda.Stream()]
+    st = [torch.cuda.Stream() for _ in range(3)]
     img = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
-    # keep the GPU warm before the first measurement
     full = lambda: L.rt_render_dev(t._ctx, ctypes.byref(cam), W, H, B, None, None, ctypes.c_void_p(img.data_ptr()),  # noqa
                                    None, None, ctypes.c_void_p(st[0].cuda_stream))
     settle(full, 0.3)
     c3_serial = event_ms(full, 40, st[0])
     for n in ns:
-        band, slab = ctypes.c_int(), ctypes.c_int()
-        abi.check(L.rt_band_plan(H, n, 0, ctypes.byref(band), ctypes.byref(slab)), "rt_band_plan")
-        hb, sr = band.value, slab.value
-        ranks = []
-        trs = [Tracer(0) for _ in range(n)]                 # one context per rank: its own view (rows) calibration
-        for r in range(n):
-            trs[r].set_scene(cfg.scene())
-            rows = abi.rt_rows(hb, n, r, 1)
-            slabs = [torch.empty((sr, W), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        for hb_req in [int(x) for x in os.environ.get("HBS", "0,8").split(",")]:
+            band, slab = ctypes.c_int(), ctypes.c_int()
+            abi.check(L.rt_band_plan(H, n, hb_req, ctypes.byref(band), ctypes.byref(slab)), "rt_band_plan")
+            hb, sr = band.value, slab.value
+            ranks = []
+            trs = [Tracer(0) for _ in range(n)]             # one context per rank: its own view (rows) calibration
+            for r in range(n):
+                trs[r].set_scene(cfg.scene())
+                rows = abi.rt_rows(hb, n, r, 1)
+                slabs = [torch.empty((sr, W), dtype=torch.uint8, device="cuda") for _ in range(3)]
 
-            def one(b, rows=rows, slabs=slabs, tr=trs[r]):
-                return L.rt_render_dev_packed(tr._ctx, ctypes.byref(cam), W, H, B, ctypes.byref(rows), abi.RT_PIXEL_GRAY32F,
-                                              None, abi.RT_PIXEL_GRAY8, ctypes.c_void_p(slabs[b].data_ptr()),
-                                              ctypes.c_void_p(st[b].cuda_stream))
-            k = [0]
+                def one(b, rows=rows, slabs=slabs, tr=trs[r]):
+                    return L.rt_render_dev_packed(tr._ctx, ctypes.byref(cam), W, H, B, ctypes.byref(rows),
+                                                  abi.RT_PIXEL_GRAY32F, None, abi.RT_PIXEL_GRAY8,
+                                                  ctypes.c_void_p(slabs[b].data_ptr()), ctypes.c_void_p(st[b].cuda_stream))
+                for b in range(3):
+                    for _ in range(3):                       # first render + calibration of this view (rows)
+                        abi.check(one(b), "first")
+                torch.cuda.synchronize()
+                rec = {"rank": r}
+                settle(full, 0.05)
+                rec["serial_ms"] = round(event_ms(lambda one=one: one(0), 40, st[0]), 5)
+                for k in (2, 3):
+                    cnt = [0]
 
-            def alt(one=one, k=k):
-                k[0] += 1
-                return one(k[0] & 1)
-            for _ in range(3):                       # first render + calibration of this view (rows)
-                abi.check(one(0), "first")
-            torch.cuda.synchronize()
-            settle(full, 0.05)
-            ser = event_ms(lambda one=one: one(0), 40, st[0])
-            settle(full, 0.05)
-            two = wall_ms(alt, 80, torch.cuda.synchronize)
-            ranks.append({"rank": r, "serial_ms": round(ser, 5), "two_streams_ms": round(two, 5)})
-        gathered = torch.zeros((n * sr, W), dtype=torch.uint8, device="cuda")
-        up = lambda: L.rt_unpack_dev(ctypes.c_void_p(gathered.data_ptr()), ctypes.c_void_p(img.data_ptr()), W, H,  # noqa
-                                     abi.RT_PIXEL_GRAY8, abi.RT_PIXEL_RGBA8, hb, n, sr, ctypes.c_void_p(st[0].cuda_stream))
-        for _ in range(5):
-            abi.check(up(), "unpack")
-        unpack = event_ms(up, 40, st[0])
-        mser = max(x["serial_ms"] for x in ranks)
-        mtwo = max(x["two_streams_ms"] for x in ranks)
-        print(json.dumps({"part": 2, "n": n, "band_height": hb, "slab_rows": sr, "c3_serial_ms": round(c3_serial, 5),
-                          "ranks": ranks, "max_serial_ms": mser, "max_two_streams_ms": mtwo,
-                          "unpack_ms": round(unpack, 5),
-                          "bound_serial": round(c3_serial / (mser + unpack), 3),
-                          "bound_two_streams": round(c3_serial / (mtwo + unpack), 3)}), flush=True)
-        for x in trs:
-            x.close()
+                    def alt(one=one, cnt=cnt, k=k):
+                        cnt[0] += 1
+                        return one(cnt[0] % k)
+                    settle(full, 0.05)
+                    rec[f"streams{k}_ms"] = round(wall_ms(alt, 120, torch.cuda.synchronize), 5)
+                ranks.append(rec)
+            gathered = torch.zeros((n * sr, W), dtype=torch.uint8, device="cuda")
+            up = lambda: L.rt_unpack_dev(ctypes.c_void_p(gathered.data_ptr()), ctypes.c_void_p(img.data_ptr()), W, H,  # noqa
+                                         abi.RT_PIXEL_GRAY8, abi.RT_PIXEL_RGBA8, hb, n, sr,
+                                         ctypes.c_void_p(st[0].cuda_stream))
+            for _ in range(5):
+                abi.check(up(), "unpack")
+            unpack = event_ms(up, 40, st[0])
+            out = {"part": 2, "n": n, "band_height": hb, "slab_rows": sr, "c3_serial_ms": round(c3_serial, 5),
+                   "unpack_ms": round(unpack, 5), "ranks": ranks}
+            for key in ("serial_ms", "streams2_ms", "streams3_ms"):
+                m = max(x[key] for x in ranks)
+                out["max_" + key] = m
+                out["bound_" + key] = round(c3_serial / (m + unpack), 3)
+            print(json.dumps(out), flush=True)
+            for x in trs:
+                x.close()
     t.close()
+
+
+def hip_runtime():
+    """The HIP runtime already loaded in this process (torch's or /opt/rocm's), by its path in /proc/self/maps."""
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64.so" in line:
+                return ctypes.CDLL(line.split()[-1])
+    raise RuntimeError("no libamdhip64 loaded")
+
+
+def make_streams(kind, k):
+    """k streams: torch's pool ("torch"), fresh non-blocking HIP streams ("hip"), or HIP streams with a full CU mask
+    ("cumask": a queue of their own in ROCclr)."""
+    hip = hip_runtime()
+    out = []
+    for _ in range(k):
+        h = ctypes.c_void_p()
+        if kind == "hip":
+            rc = hip.hipStreamCreateWithFlags(ctypes.byref(h), 1)
+        else:
+            mask = (ctypes.c_uint32 * 8)(*([0xFFFFFFFF] * 8))        # 256 CUs
+            rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), 8, mask)
+        assert rc == 0, rc
+        out.append(h.value)
+    return out
+
+
+def part3():
+    """Frames in flight over K streams of each kind: c2 full frames (the bench's pattern) and c4 rank band sets at
+    N = 8 (band height 8), one context per stream slot."""
+    kinds = os.environ.get("KINDS", "torch,hip,cumask").split(",")
+    c2 = scenes.CONFIGS["c2"]
+    for kind in kinds:
+        for k in (1, 2, 3, 4):
+            if kind == "torch":
+                ts = [torch.cuda.Stream() for _ in range(k)]
+                handles = [s.cuda_stream for s in ts]
+            else:
+                handles = make_streams(kind, k)
+            for wl in ("c2", "c4r3"):
+                if wl == "c2":
+                    Wc, Hc, Bc, cm, sc, rows = c2.width, c2.height, c2.depth, c2.camera(), c2.scene(), None
+                    npx = Hc
+                else:
+                    Wc, Hc, Bc, cm, sc = W, H, B, cam, cfg.scene()
+                    rows = abi.rt_rows(8, 8, 3, 1)
+                    npx = 272
+                trs = [Tracer(0) for _ in range(k)]
+                outs = []
+                for tt in trs:
+                    tt.set_scene(sc)
+                    if wl == "c2":                       # the bench's outputs: RGBA32F + RGBA8
+                        outs.append((torch.empty((npx, Wc, 4), dtype=torch.float32, device="cuda"),
+                                     torch.empty((npx, Wc, 4), dtype=torch.uint8, device="cuda")))
+                    else:
+                        outs.append((None, torch.empty((npx, Wc), dtype=torch.uint8, device="cuda")))
+                fmt = (abi.RT_PIXEL_RGBA32F, abi.RT_PIXEL_RGBA8) if wl == "c2" else (abi.RT_PIXEL_GRAY32F, abi.RT_PIXEL_GRAY8)
+                la = [(trs[q]._ctx, ctypes.byref(cm), Wc, Hc, Bc, ctypes.byref(rows) if rows else None,
+                       fmt[0], ctypes.c_void_p(outs[q][0].data_ptr()) if outs[q][0] is not None else None,
+                       fmt[1], ctypes.c_void_p(outs[q][1].data_ptr()), ctypes.c_void_p(handles[q])) for q in range(k)]
+                for a in la:
+                    for _ in range(3):
+                        abi.check(L.rt_render_dev_packed(*a), "first")
+                torch.cuda.synchronize()
+                cnt = [0]
+
+                def f(la=la, cnt=cnt, k=k):
+                    cnt[0] += 1
+                    return L.rt_render_dev_packed(*la[cnt[0] % k])
+                settle(f, 0.2)
+                ms = statistics.median(wall_ms(f, 200, torch.cuda.synchronize) for _ in range(5))
+                print(json.dumps({"part": 3, "stream_kind": kind, "streams": k, "workload": wl,
+                                  "ms_per_frame": round(ms, 5)}), flush=True)
+                for tt in trs:
+                    tt.close()
+
+
+def part4():
+    """rank 0's unpack alone: an n-rank gathered GRAY8 (and RGB8) c4 buffer into the RGBA8 image."""
+    st = torch.cuda.Stream()
+    img = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+    for n, hb_req in ((8, 8), (8, 0), (4, 0), (2, 0)):
+        band, slab = ctypes.c_int(), ctypes.c_int()
+        abi.check(L.rt_band_plan(H, n, hb_req, ctypes.byref(band), ctypes.byref(slab)), "rt_band_plan")
+        hb, sr = band.value, slab.value
+        out = {"part": 4, "n": n, "band_height": hb, "unpack_vec4_env": os.environ.get("RT_UNPACK_VEC4")}
+        for fmt, ch in ((abi.RT_PIXEL_GRAY8, 1), (abi.RT_PIXEL_RGB8, 3)):
+            gathered = torch.zeros((n * sr, W * ch), dtype=torch.uint8, device="cuda")
+            up = lambda: L.rt_unpack_dev(ctypes.c_void_p(gathered.data_ptr()), ctypes.c_void_p(img.data_ptr()), W, H,  # noqa
+                                         fmt, abi.RT_PIXEL_RGBA8, hb, n, sr, ctypes.c_void_p(st.cuda_stream))
+            settle(up, 0.1)
+            out["gray8_ms" if ch == 1 else "rgb8_ms"] = round(statistics.median(event_ms(up, 100, st) for _ in range(5)), 5)
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
@@ -172,3 +273,7 @@ if __name__ == "__main__":
         part1(int(os.environ.get("ROUNDS", "3")))
     if "2" in parts:
         part2([int(x) for x in os.environ.get("NS", "2,4,8").split(",")])
+    if "3" in parts:
+        part3()
+    if "4" in parts:
+        part4()
