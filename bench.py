@@ -338,25 +338,28 @@ def c4_scaling_keys(n, W, H, rays, c4_ms, c3_ms_inflight, c3_ms_serial):
 XGMI_LINK_GBS = 153.0                                   # nominal per-link rate (7 links per MI355X); not measured here
 
 
-def c4_projection_keys(n, c3_ms_per_frame, rank_ms, unpack_ms, slab_bytes):
+def c4_projection_keys(n, c3_ms_per_frame, rank_ms, unpack_ms, slab_bytes, root_ms=None):
     """One GPU's projection of an n-rank c4 frame (rt_render_multi at n ranks cannot run on one GPU): every rank's band
     set rendered alone the way the group renders it (rank_ms[r], per frame, frames in flight as the group keeps them),
-    and rank 0's unpack of the n-rank gathered buffer.  Rank 0 renders its bands and unpacks on one GPU, so the
-    projected frame interval is max(rank_ms) + unpack_ms (the unpack counted in full, although it runs on rank 0's
-    high-priority stream beside the next render); the gather itself (each peer's slab_bytes over its own xGMI link into
-    rank 0, double-buffered behind the next render) is reported at the nominal link rate, not measured, and bounds the
-    interval only if it is the longest stage."""
+    and rank 0's unpack of the n-rank gathered buffer (unpack_ms, alone).  root_ms: rank 0's own pipeline measured as
+    the group runs it — its bands on the render streams and, per frame, the unpack on its high-priority comm stream
+    behind that frame's render — so the unpack overlaps the next render; without it rank 0 is charged its render plus
+    the whole unpack.  Projected frame interval = the slowest stage: max(rank_ms[1:], rank 0), or the gather (each
+    peer's slab_bytes over its own xGMI link into rank 0, double-buffered behind the next render) at the nominal link
+    rate — not measured — when that is longer."""
     render = max(rank_ms)
-    frame = render + unpack_ms
+    root = root_ms if root_ms is not None else rank_ms[0] + unpack_ms
+    frame = max(max(rank_ms[1:], default=0.0), root)
     xfer = slab_bytes / (XGMI_LINK_GBS * 1e9) * 1e3
     bound = max(frame, xfer)
     key = f"n{n}"
-    return {f"{key}_rank_render_ms": [round(x, 5) for x in rank_ms], f"{key}_rank_render_ms_max": round(render, 5),
-            f"{key}_unpack_ms": round(unpack_ms, 5), f"{key}_projected_frame_ms": round(bound, 5),
-            f"{key}_gather_ms_nominal": round(xfer, 5),
-            f"{key}_limiting_stage": ("gather (nominal xGMI)" if xfer > frame else
-                                      "rank render" if render >= unpack_ms else "unpack"),
-            f"{key}_speedup_bound": round(c3_ms_per_frame / bound, 3)}
+    out = {f"{key}_rank_render_ms": [round(x, 5) for x in rank_ms], f"{key}_rank_render_ms_max": round(render, 5),
+           f"{key}_unpack_ms": round(unpack_ms, 5), f"{key}_rank0_ms": round(root, 5),
+           f"{key}_projected_frame_ms": round(bound, 5), f"{key}_gather_ms_nominal": round(xfer, 5),
+           f"{key}_limiting_stage": ("gather (nominal xGMI)" if xfer > frame else
+                                     "rank 0 (bands + unpack)" if root >= frame else "a peer's band render"),
+           f"{key}_speedup_bound": round(c3_ms_per_frame / bound, 3)}
+    return out
 
 
 def c4_parallelism_text(n, c4):
@@ -439,7 +442,42 @@ def c4_rank_projection(torch, L, abi, Tracer, cfg, dev, local, n, band_height, c
         abi.check(L.rt_unpack_dev(*ua), "rt_unpack_dev")
     e[1].record(sts[0])
     torch.cuda.synchronize()
-    keys = c4_projection_keys(n, c3_ms_per_frame, rank_ms, e[0].elapsed_time(e[1]) / 40, sr * W)
+    unpack_ms = e[0].elapsed_time(e[1]) / 40
+    # rank 0 as rt_render_multi runs it: bands on the two render streams in turn, each frame's unpack (its slab and the
+    # gathered peers' bands, pre-filled) on a high-priority comm stream behind that frame's render
+    t = Tracer(local)
+    t.set_scene(cfg.scene())
+    rows = abi.rt_rows(hb, n, 0, 1)
+    gath = [torch.zeros((n * sr, W), dtype=torch.uint8, device=dev) for _ in range(2)]
+    cs = torch.cuda.Stream(dev, priority=-1)
+    ev_r = [torch.cuda.Event() for _ in range(2)]
+    ev_a = [torch.cuda.Event() for _ in range(2)]
+    la = [(t._ctx, ctypes.byref(cam), W, H, B, ctypes.byref(rows), abi.RT_PIXEL_GRAY32F, None, abi.RT_PIXEL_GRAY8,
+           ctypes.c_void_p(gath[k].data_ptr()), ctypes.c_void_p(sts[k].cuda_stream)) for k in range(2)]
+    ub = [(ctypes.c_void_p(gath[k].data_ptr()), ctypes.c_void_p(img.data_ptr()), W, H, abi.RT_PIXEL_GRAY8,
+           abi.RT_PIXEL_RGBA8, hb, n, sr, ctypes.c_void_p(cs.cuda_stream)) for k in range(2)]
+    used = [False, False]
+
+    def root_frame(f):
+        k = f & 1
+        if used[k]:
+            sts[k].wait_event(ev_a[k])                        # frame f - 2's unpack has read slab k
+        abi.check(L.rt_render_dev_packed(*la[k]), "rt_render_dev_packed")
+        ev_r[k].record(sts[k])
+        cs.wait_event(ev_r[k])
+        abi.check(L.rt_unpack_dev(*ub[k]), "rt_unpack_dev")
+        ev_a[k].record(cs)
+        used[k] = True
+    for f in range(3 + frames // 2):
+        root_frame(f)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for f in range(frames):
+        root_frame(f)
+    torch.cuda.synchronize()
+    root_ms = (time.perf_counter() - t0) * 1e3 / frames
+    t.close()
+    keys = c4_projection_keys(n, c3_ms_per_frame, rank_ms, unpack_ms, sr * W, root_ms=root_ms)
     keys[f"n{n}_band_height"] = hb
     return keys
 
@@ -1047,9 +1085,11 @@ def main() -> int:
                                                        base[0]))
                     proj["note"] = ("one-GPU projection of the c4 frame at n ranks (rt_render_multi at n > 1 needs n "
                                     "GPUs): nN_rank_render_ms = each rank's band set rendered alone as the group "
-                                    "renders it (GRAY8 slab, two render streams taking frames in turn), "
-                                    "nN_projected_frame_ms = the slowest rank + rank 0's unpack of the gathered GRAY8 "
-                                    "buffer (or the nominal xGMI gather of one slab if longer), nN_speedup_bound = "
+                                    "renders it (GRAY8 slab, two render streams taking frames in turn); nN_rank0_ms "
+                                    "= rank 0's pipeline as the group runs it (its bands, then per frame the unpack of "
+                                    "the gathered GRAY8 buffer into RGBA8 on a high-priority stream beside the next "
+                                    "render); nN_projected_frame_ms = the slowest of rank 0 and the peers (or the "
+                                    "nominal xGMI gather of one slab if longer); nN_speedup_bound = "
                                     "c3_1gpu_ms_per_frame / nN_projected_frame_ms")
                     info["projection"] = proj
                 info["scaling_note"] = ("speedup_vs_c3_1gpu = c3_1gpu_ms_per_frame (one GPU, RGBA8 only, "

@@ -131,14 +131,18 @@ def test_cpu_baseline_labels_threads_not_cores():
 
 
 def test_c4_projection_keys():
-    """The one-GPU projection of the 8-rank c4 frame: slowest rank's band render + rank 0's unpack, or the nominal
-    gather when that is longer; speed-up bound against the one-GPU c3 frame."""
+    """The one-GPU projection of the 8-rank c4 frame: the slowest of rank 0's pipeline (its bands + unpack, measured
+    or, without it, summed) and the peers' band renders, or the nominal gather when longer; speed-up bound against
+    the one-GPU c3 frame."""
     k = bench.c4_projection_keys(8, 0.112, [0.015, 0.0165, 0.016], 0.003, 1_044_480)
     assert k["n8_rank_render_ms_max"] == 0.0165 and k["n8_unpack_ms"] == 0.003
-    assert k["n8_projected_frame_ms"] == round(0.0165 + 0.003, 5)
-    assert k["n8_speedup_bound"] == round(0.112 / 0.0195, 3)
-    assert k["n8_limiting_stage"] == "rank render"
+    assert k["n8_rank0_ms"] == 0.018 and k["n8_projected_frame_ms"] == 0.018
+    assert k["n8_speedup_bound"] == round(0.112 / 0.018, 3)
+    assert k["n8_limiting_stage"] == "rank 0 (bands + unpack)"
     assert abs(k["n8_gather_ms_nominal"] - 1_044_480 / 153e9 * 1e3) < 1e-5
+    m = bench.c4_projection_keys(8, 0.112, [0.015, 0.0165, 0.016], 0.003, 1_044_480, root_ms=0.016)
+    assert m["n8_projected_frame_ms"] == 0.0165 and m["n8_limiting_stage"] == "a peer's band render"
+    assert m["n8_speedup_bound"] == round(0.112 / 0.0165, 3)
     slow = bench.c4_projection_keys(8, 0.112, [0.001], 0.0005, 10_000_000)      # gather-bound
     assert slow["n8_limiting_stage"] == "gather (nominal xGMI)"
     assert slow["n8_projected_frame_ms"] == slow["n8_gather_ms_nominal"]

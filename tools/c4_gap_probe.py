@@ -267,6 +267,44 @@ def part4():
         print(json.dumps(out), flush=True)
 
 
+def part5():
+    """Which hardware queues frames in flight land on (run under rocprofv3 --kernel-trace: Queue_Id per dispatch): for
+    each stream kind, 3 streams taking 30 c2 frames in turn, kinds separated by 50 ms idle gaps; also prints each kind's
+    per-frame interval over 200 frames."""
+    c2 = scenes.CONFIGS["c2"]
+    Wc, Hc, Bc, cm = c2.width, c2.height, c2.depth, c2.camera()
+    for kind in os.environ.get("KINDS", "torch,hip,cumask,prio").split(","):
+        if kind == "torch":
+            handles = [torch.cuda.Stream().cuda_stream for _ in range(3)]
+        elif kind == "prio":                                    # one stream per priority level
+            handles = [torch.cuda.Stream(priority=p).cuda_stream for p in (0, -1, -2)]
+        else:
+            handles = make_streams(kind, 3)
+        trs = [Tracer(0) for _ in range(3)]
+        outs = []
+        for tt in trs:
+            tt.set_scene(c2.scene())
+            outs.append((torch.empty((Hc, Wc, 4), dtype=torch.float32, device="cuda"),
+                         torch.empty((Hc, Wc, 4), dtype=torch.uint8, device="cuda")))
+        la = [(trs[q]._ctx, ctypes.byref(cm), Wc, Hc, Bc, None, ctypes.c_void_p(outs[q][0].data_ptr()),
+               ctypes.c_void_p(outs[q][1].data_ptr()), None, None, ctypes.c_void_p(handles[q])) for q in range(3)]
+        for a in la:
+            for _ in range(3):
+                abi.check(L.rt_render_dev(*a), "first")
+        cnt = [0]
+
+        def f(la=la, cnt=cnt):
+            cnt[0] += 1
+            return L.rt_render_dev(*la[cnt[0] % 3])
+        settle(f, 0.1)
+        time.sleep(0.05)
+        ms = statistics.median(wall_ms(f, 200, torch.cuda.synchronize) for _ in range(3))
+        time.sleep(0.05)
+        print(json.dumps({"part": 5, "stream_kind": kind, "ms_per_frame": round(ms, 5)}), flush=True)
+        for tt in trs:
+            tt.close()
+
+
 if __name__ == "__main__":
     parts = os.environ.get("PARTS", "1,2").split(",")
     if "1" in parts:
@@ -277,3 +315,5 @@ if __name__ == "__main__":
         part3()
     if "4" in parts:
         part4()
+    if "5" in parts:
+        part5()
