@@ -1231,6 +1231,21 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
     *pe = add(p, r);                                        // Line(p, p + r)
 }
 
+// Per-tile cache of the culling masks of every level (r06, RT_LEVEL_MASKS): a static view's rays are the same bits in
+// every frame, so the wave-uniform masks ray_bundle_mask and shadow_bundle_mask compute from them are a pure function
+// of the view, like the primary cone mask of the dispatch record.  The view's calibration render stores them per tile
+// (`out`, lane 0), later renders of exactly that view read them (`in`) instead of computing them: slot l - 1 holds
+// level l's ray mask (l = 1 .. B), slot B + l nl + i the shadow mask of light i at level l.  A mask is stored only
+// where the wave computes it (a level every lane missed before is never reached, in either render).  Both null: the
+// masks are computed (moving cameras, the calibration's first render, scenes with too many slots).  The wave keeps
+// only its tile's first slot; the two arrays' addresses are read from the kernel arguments where a mask is needed
+// (level_masks_in / _out, rt_render.hpp), so no pointer is held in SGPRs through the trace.
+struct LevelMasks {
+    int tile;                                  // first slot of this wave's tile (tile * slots per tile), -1: none
+};
+__device__ __forceinline__ const uint64_t* level_masks_in();
+__device__ __forceinline__ uint64_t* level_masks_out();
+
 // Local illumination of one hit over all lights (:1213-1228).  ks = |u . rdir|, u = incoming ray
 // direction, rdir = reflectedRay().direction() (:1225).  `hit` marks the lanes whose colour is wanted.  CULL: called by all
 // lanes of the wave, the light loop stays converged for shadow_bundle_mask; otherwise only by hit lanes.
@@ -1245,7 +1260,8 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
 // (R, R, R) — bit for bit the reference's (G and B are R's operations repeated).  Not with FULL (transparency weights).
 template <bool FULL, bool CULL, bool ACC = false, int SS = 256, bool ACHRO = false>
 __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, int mat, double ks,
-                                    int skip = -1, double* acc = nullptr) {
+                                    int skip = -1, double* acc = nullptr, const LevelMasks* lm = nullptr,
+                                    int lslot = 0) {
     static_assert(!(ACHRO && FULL), "achromatic shading is for opaque scenes");
     const DevScene* S = V.S;
     d3 color = mk(0.0, 0.0, 0.0);
@@ -1267,7 +1283,18 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
         set_dir(&sr, sd, sdir);
         const double kd = fabs(dot(n, sdir));               // before the shadow test: fewer live registers
         uint64_t m = ~0ull;
-        if (CULL && !FULL && V.np >= kConeMin) m = shadow_bundle_mask(V, hit, sr, i);
+        if (CULL && !FULL && V.np >= kConeMin) {
+            // (light i's shadow mask at this level: cached per tile for a calibrated static view, LevelMasks)
+            const int t = lm ? lm->tile : -1;
+            const uint64_t* in = t >= 0 ? level_masks_in() : nullptr;
+            if (in) {
+                m = in[t + lslot + i];
+            } else {
+                m = shadow_bundle_mask(V, hit, sr, i);
+                uint64_t* out = t >= 0 ? level_masks_out() : nullptr;
+                if (out && __lane_id() == 0) out[t + lslot + i] = m;
+            }
+        }
         bool lit = false;
         if (hit) lit = !(FULL ? occluded_transparent(V, sr) : occluded<false, CULL>(V, sr, i, m, skip));
         if (lit && ACHRO) {                                 // R only (same operations as below, channel x)
@@ -1393,7 +1420,8 @@ __device__ __forceinline__ void next_ray(d3 p, d3 nd, d3 nu, Ray* r) {
 // shadow_bundle_mask reduce over it).  Returns false when no lane hit (the bounce loop ends).
 template <int B, bool TRANSP, int SS = kSlotStride, bool ACHRO = false>
 __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool first, bool alive, uint64_t cone, Ray* r, int* levels,
-                                           double* slot, int* mslot, int* skip, bool lazy_u, d3* last) {
+                                           double* slot, int* mslot, int* skip, bool lazy_u, d3* last,
+                                           const LevelMasks& lm) {
     // the last level's colour stays in registers (RT_CULL_LAST_REG): slot B does not exist, so the continuation
     // of level B - 1 parks only its end - start and recomputes its unit direction after the light loop
     constexpr bool kLastReg = RT_CULL_LAST_REG && !TRANSP;
@@ -1401,7 +1429,16 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     RT_COUNT(V.S, kCntLevels, 1);
     if (!first) {
         set_origin_f32(V.S, r);
-        if (V.np >= kConeMin) smask = ray_bundle_mask(V, alive, *r);
+        if (V.np >= kConeMin) {
+            const uint64_t* in = lm.tile >= 0 ? level_masks_in() : nullptr;
+            if (in) {
+                smask = in[lm.tile + lvl - 1];              // this tile's level-lvl ray mask (calibrated view)
+            } else {
+                smask = ray_bundle_mask(V, alive, *r);
+                uint64_t* out = lm.tile >= 0 ? level_masks_out() : nullptr;
+                if (out && __lane_id() == 0) out[lm.tile + lvl - 1] = smask;
+            }
+        }
     }
     d3 p = mk(0.0, 0.0, 0.0);
     int kind = -1;
@@ -1442,7 +1479,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
             asm volatile("" ::: "memory");
         }
     }
-    const d3 c = shade<TRANSP, true, false, 256, ACHRO>(V, hit, p, n, mat, ks, *skip);
+    const d3 c = shade<TRANSP, true, false, 256, ACHRO>(V, hit, p, n, mat, ks, *skip, nullptr, &lm, B + lvl * V.nl);
     d3 nu = nd;
     if (hit) {
         if (kParkCull && lvl < B) {
@@ -1465,7 +1502,8 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
 
 template <int B, bool PRIMARY, bool TRANSP, bool CULL, int SS = kSlotStride, bool ACHRO = false>
 __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t cone,
-                                    uint32_t* seg, uint32_t* shadow, double* slot, int* mslot) {
+                                    uint32_t* seg, uint32_t* shadow, double* slot, int* mslot,
+                                    LevelMasks lm = LevelMasks{-1}) {
     const DevScene* S = V.S;
     int levels = 0;
     Ray r;
@@ -1495,7 +1533,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t c
         const bool first = PRIMARY && lvl == 0;
         if (CULL) {
             if (!cull_level<B, TRANSP, SS, ACHRO>(V, lvl, first, alive, cone, &r, &levels, slot, mslot,
-                                           &skip, lazy_u, &last))
+                                           &skip, lazy_u, &last, lm))
                 break;
         } else {
             d3 p = mk(0.0, 0.0, 0.0);

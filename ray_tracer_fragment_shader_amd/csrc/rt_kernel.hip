@@ -522,6 +522,13 @@ struct rt_ctx {
     // tracking below.
     uint64_t* d_cone_tile = nullptr;
     bool cone_valid = false;                   // d_disp holds the masks of view order_key
+    // r06: the culling kernels' level masks of view order_key, lmask_stride per tile (rt_device.hpp LevelMasks),
+    // written by its calibration render (grow-only, lmask_cap masks); RT_LEVEL_MASKS=0: computed in every render
+    uint64_t* d_lmask = nullptr;
+    size_t lmask_cap = 0;
+    int lmask_stride = 0;
+    bool lmask_valid = false;
+    bool level_masks = true;
     // Cross-stream ordering of the per-view state: the per-eye records inside d_scene (rt_prepare_kernel) and the
     // calibration buffers (d_row_cost, d_tile_rows, d_tile_cost, d_cone_tile, d_disp).  Every render reads the per-eye
     // records; a render that prepares a new eye or calibrates also writes.  A writer records view_ev on its stream
@@ -667,6 +674,7 @@ extern "C" int rt_ctx_destroy(rt_ctx* c) {
     if (c->d_tile_rows) (void)hipFree(c->d_tile_rows);
     if (c->d_row_cost) (void)hipFree(c->d_row_cost);
     rt_free_view_bufs(c);
+    if (c->d_lmask) (void)hipFree(c->d_lmask);
     if (c->sd_ok) {
         for (int b = 0; b < rt_ctx::kSlots; ++b) {
             (void)sdma_wait(c, b);                     // (the render stream has drained: its signal has fired)
@@ -713,6 +721,7 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_COPY_BLOCKS")) c->copy_blocks = std::max(atoi(e), 0);
     if (const char* e = getenv("RT_COPY_KERNEL")) c->copy_kernel = std::min(std::max(atoi(e), -1), 1);
     if (const char* e = getenv("RT_CONE_CACHE")) c->cone_cache = atoi(e) != 0;
+    if (const char* e = getenv("RT_LEVEL_MASKS")) c->level_masks = atoi(e) != 0;
     if (const char* e = getenv("RT_ORDER_POLICY")) c->order_policy = std::min(std::max(atoi(e), 0), 1);
     if (const char* e = getenv("RT_ACHRO_OFF")) c->achro_off = atoi(e) != 0;
     if (hipMalloc(&c->d_tile_rows, sizeof(int32_t) * kOrderMax) != hipSuccess ||
@@ -887,7 +896,11 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
     RT_HIP(hipStreamIsCapturing(st, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
     if (capturing) c->ever_captured = true;
-    bool calibrate = false, cone_calib = false;
+    bool calibrate = false, cone_calib = false, lm_calib = false;
+    // level masks per tile (culling kernels of opaque scenes, one-wave tiles): B ray masks + (B + 1) nl shadow masks
+    const bool cull_kernel = c->n_padded >= kConeMin && !c->tree && !c->transparent && !big && RT_WG_FAST == 64;
+    int lm_stride = cull_kernel && c->level_masks && c->cone_cache ? depth + (depth + 1) * c->n_lights : 0;
+    if (lm_stride > kLevelMaskSlotsMax) lm_stride = 0;
     rt_ctx::ViewKey key{};
     // (dispatch records pack the tile as ty << 16 | tx)
     if (!capturing && c->order_mode == 0 && tiles_y <= c->n_tile_rows && tiles_x < 65536 && tiles_y < 65536) {
@@ -910,6 +923,10 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
             P.disp = c->d_disp;
             // (the cached masks hold one mask per one-wave 8 x 8 tile: the 256-thread A/B variants never read them)
             P.cone_use = c->cone_valid && !big ? 1 : 0;
+            if (c->lmask_valid && lm_stride > 0 && c->lmask_stride == lm_stride) {   // this view's level masks
+                P.lmask_in = c->d_lmask;
+                P.lmask_stride = lm_stride;
+            }
         } else if (same_shape) {
             P.disp = c->d_disp;                         // another camera: the last calibrated order, its own masks
             if (++c->stale >= kRecalibrate) {           // ... re-timed every kRecalibrate-th render
@@ -922,6 +939,7 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
             // the calibration records one mask per tile from lane 0 of its wave: one-wave workgroups only
             cone_calib = c->cone_cache && c->n_padded >= kPrimaryConeMin && !c->tree && !c->transparent && !big &&
                          RT_WG_FAST == 64;
+            lm_calib = cone_calib && lm_stride > 0;
         } else {
             c->seen_key = key;                          // first render of this view: identity order
             c->seen_valid = true;
@@ -934,7 +952,8 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
         if (c->view_rec && c->view_st != st) RT_HIP(hipStreamWaitEvent(st, c->view_ev, 0));
         if (prepare || calibrate) {
             // write-after-read: renders queued on other streams may still read what this render rewrites (or frees)
-            if ((c->readers && (c->readers_multi || c->reader_st != st)) || (calibrate && tiles > c->view_cap))
+            if ((c->readers && (c->readers_multi || c->reader_st != st)) || (calibrate && tiles > c->view_cap) ||
+                (lm_calib && tiles * (size_t)lm_stride > c->lmask_cap))
                 RT_HIP(hipDeviceSynchronize());
             c->readers = c->readers_multi = false;      // same-stream renders are ordered before the rewrite
         }
@@ -949,13 +968,29 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
         // the calibration render writes every tile's wave time (and, a static view's, its cone mask); the buffers
         // grow here (the device was drained above)
         c->cone_valid = false;
+        c->lmask_valid = false;
         if (!rt_grow_view_bufs(c, tiles)) {             // out of memory: identity order, masks in the kernel
-            calibrate = cone_calib = false;
+            calibrate = cone_calib = lm_calib = false;
             P.disp = nullptr;
             P.cone_use = 0;
         } else {
             P.tile_cost = c->d_tile_cost;
             if (cone_calib) P.cone_out = c->d_cone_tile;
+        }
+        if (lm_calib && tiles * (size_t)lm_stride > c->lmask_cap) {     // (the device was drained above)
+            if (c->d_lmask) (void)hipFree(c->d_lmask);
+            c->d_lmask = nullptr;
+            c->lmask_cap = 0;
+            if (hipMalloc(&c->d_lmask, tiles * (size_t)lm_stride * sizeof(uint64_t)) == hipSuccess)
+                c->lmask_cap = tiles * (size_t)lm_stride;
+            else
+                (void)hipGetLastError();                // out of memory: the masks stay in the kernel
+        }
+        if (lm_calib && c->d_lmask) {
+            P.lmask_out = c->d_lmask;
+            P.lmask_stride = lm_stride;
+        } else {
+            lm_calib = false;
         }
     }
     const dim3 grid((unsigned)tiles_x, (unsigned)std::min(tiles_y, kGridY), (unsigned)((tiles_y + kGridY - 1) / kGridY));
@@ -1042,6 +1077,8 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
         c->order_key = key;                             // only once the order kernel is queued
         c->order_valid = true;
         c->cone_valid = cone_calib;
+        c->lmask_valid = lm_calib;
+        c->lmask_stride = lm_calib ? lm_stride : 0;
         c->stale = 0;
     }
     if ((prepare || calibrate) && !capturing) {

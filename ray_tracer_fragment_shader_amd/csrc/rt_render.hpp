@@ -71,6 +71,12 @@ __host__ __device__ constexpr int kDefaultMinWaves(int B) { return B <= 2 ? 6 : 
 #ifndef RT_MAX_B
 #define RT_MAX_B 7
 #endif
+// Per-tile cache of the culling kernels' level masks (rt_device.hpp LevelMasks); 0: always computed (A/B builds).
+#ifndef RT_LEVEL_MASKS
+#define RT_LEVEL_MASKS 1
+#endif
+// The most mask slots per tile the cache holds (B ray masks + (B + 1) nl shadow masks); beyond it the masks are computed.
+constexpr int kLevelMaskSlotsMax = 24;
 
 namespace rtk {
 
@@ -157,6 +163,11 @@ struct RenderParams {
     int32_t cone_use;                          // 1: disp's cone masks are this view's (cached primary cone masks)
     uint64_t* cone_out;                        // calibration render: each tile's mask, by tile (or nullptr)
     int32_t ns;                                // stride of the scene's per-sphere arrays (DevScene::n_stride)
+    // Per-tile level masks (rt_device.hpp LevelMasks; culling kernels, one-wave tiles): lmask_stride slots per tile,
+    // written by the calibration render (lmask_out) and read by later renders of exactly that view (lmask_in)
+    uint64_t* lmask_out;
+    const uint64_t* lmask_in;
+    int32_t lmask_stride;
 };
 
 // The dispatch table's geometry, scalar arguments right after the table, so that gfx950's kernarg preload
@@ -203,6 +214,31 @@ __device__ __forceinline__ RenderOuts late_outputs() {
     o.orc = (uint32_t*)*(kpp)(ka + offsetof(RenderArgs, orc));
     return o;
 }
+
+}  // namespace rtk
+
+// The level-mask arrays of the render (RenderParams::lmask_in / lmask_out, rt_device.hpp LevelMasks), read from the
+// kernel-argument segment where a mask is needed (behind an opaque copy of the segment pointer, as late_outputs).
+namespace rt {
+using rtk::RenderArgs;
+using rtk::RenderParams;
+__device__ __forceinline__ const uint64_t* level_masks_in() {
+    typedef const __attribute__((address_space(4))) char* kptr;
+    typedef const uint64_t* const __attribute__((address_space(4)))* kpp;
+    kptr ka = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    return *(kpp)(ka + offsetof(RenderArgs, P) + offsetof(RenderParams, lmask_in));
+}
+__device__ __forceinline__ uint64_t* level_masks_out() {
+    typedef const __attribute__((address_space(4))) char* kptr;
+    typedef uint64_t* const __attribute__((address_space(4)))* kpp;
+    kptr ka = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    return *(kpp)(ka + offsetof(RenderArgs, P) + offsetof(RenderParams, lmask_out));
+}
+}  // namespace rt
+
+namespace rtk {
 
 // Image row (within its frame) of local row lr; local rows are frame-major (rt_rows.frames).
 __device__ __forceinline__ int global_row_of(const RenderParams& P, int lr) {
@@ -377,10 +413,12 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     const uint64_t t_mid = __builtin_amdgcn_s_memrealtime();   // prologue done: the primary ray is formed
 #endif
     d3 col;
+    LevelMasks lm{-1};
+    if (CULL && RT_LEVEL_MASKS && P.lmask_stride > 0 && !pad) lm.tile = (ty * P.tiles_x + tx) * P.lmask_stride;
     if constexpr (TREE)
         col = trace_tree<B>(V, eye, sp, &seg, &sh);
     else
-        col = trace<B, true, TRANSP, CULL, WG, ACHRO>(V, eye, sp, cone, &seg, &sh, slot, mslot);
+        col = trace<B, true, TRANSP, CULL, WG, ACHRO>(V, eye, sp, cone, &seg, &sh, slot, mslot, lm);
 #if RT_WAVE_TRACE >= 2
     asm volatile("" ::"v"(col.x), "v"(col.y), "v"(col.z));
     const uint64_t t_trace = __builtin_amdgcn_s_memrealtime();   // trace() done, the stores next

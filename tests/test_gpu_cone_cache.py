@@ -169,3 +169,71 @@ def test_calibrate_on_one_stream_read_on_another(name):
             fresh.close()
     finally:
         t.close()
+
+
+def _random_cull_scene(rng, n_spheres, n_lights):
+    sq = [chr(ord("a") + int(rng.integers(0, 8))) + chr(ord("1") + int(rng.integers(0, 8))) for _ in range(n_spheres)]
+    sph = [scenes.SphereSpec(s, float(rng.uniform(2, 30)), float(rng.uniform(-40, 90))) for s in sq]
+    lts = [scenes.LightSpec(chr(ord("a") + int(rng.integers(0, 8))) + chr(ord("1") + int(rng.integers(0, 8))),
+                            scenes.WHITE if k % 2 == 0 else tuple(float(x) for x in rng.uniform(0, 1, 3)))
+           for k in range(n_lights)]
+    return scenes.Scene(spheres=sph, lights=lts)
+
+
+@pytest.mark.parametrize("seed,n_spheres,n_lights,depth", [(0, 20, 1, 2), (1, 40, 2, 3), (2, 64, 3, 5),
+                                                           (3, 33, 2, 7), (4, 48, 4, 5)])
+def test_level_mask_cache_random_culling_scenes(seed, n_spheres, n_lights, depth):
+    """The culling kernels' per-tile level masks (rt_device.hpp LevelMasks): the calibration render of a static view
+    stores every level's ray and shadow masks, later renders of that view read them instead of computing them.  Random
+    scenes of >= 16 spheres (the culling kernels), 1-4 lights, depth 2-7 — including slot counts past the cache's
+    limit (seed 3: 7 + 8 x 2 = 23 slots, cached; seed 4: 5 + 6 x 4 = 29, computed): the first, calibration and cached
+    renders, and a context with the cache off (RT_LEVEL_MASKS=0), all equal the oracle bit for bit."""
+    rng = np.random.default_rng(seed)
+    sc = _random_cull_scene(rng, n_spheres, n_lights)
+    W, H = 160, 120
+    cam = scenes.make_camera(W, H, float(rng.uniform(1.0, 3.0)))
+    want, want_rc = po.render(sc.to_abi(), cam, W, H, depth)
+    t = Tracer(0)
+    try:
+        t.set_scene(sc)
+        for k in range(5):
+            b = t.render(cam, W, H, depth, rgba32f=False, rgb64f=True, raycount=True)
+            torch.cuda.synchronize()
+            assert np.array_equal(b["rgb64f"].cpu().numpy(), want, equal_nan=True), f"render {k}"
+            assert np.array_equal(b["raycount"].cpu().numpy().view(np.uint32), want_rc), f"render {k}"
+        # the bench's output set (RGBA32F + RGBA8): its own calibration and cached renders equal the first
+        first = t.render(cam, W, H, depth, rgba32f=True, rgba8=True)
+        torch.cuda.synchronize()
+        ref = (first["rgba32f"].clone(), first["rgba8"].clone())
+        for k in range(3):
+            b = t.render(cam, W, H, depth, rgba32f=True, rgba8=True)
+            torch.cuda.synchronize()
+            assert torch.equal(b["rgba32f"], ref[0]) and torch.equal(b["rgba8"], ref[1]), f"rgba render {k}"
+    finally:
+        t.close()
+
+
+def test_level_mask_cache_off_and_view_changes(monkeypatch):
+    """c5 (64 spheres, 2 lights, depth 3) at 640x360: a context without the level-mask cache (RT_LEVEL_MASKS=0) and one
+    with it render the same frames; then the cached context renders another camera (masks computed in the kernel, the
+    calibrated order reused) and the cached view again — every frame equals the uncached context's."""
+    cfg = scenes.CONFIGS["c5"]
+    W, H = 640, 360
+    monkeypatch.setenv("RT_LEVEL_MASKS", "0")
+    off = Tracer(0)
+    monkeypatch.delenv("RT_LEVEL_MASKS")
+    on = Tracer(0)
+    try:
+        for t in (off, on):
+            t.set_scene(cfg.scene())
+        cams = [cfg.camera(W, H), cfg.camera(W, H)]
+        cams[1].eye = abi.vec3((60.0 * np.sin(0.7), 100.0 + 10.0 * np.cos(0.7), 200.0))
+        seq = [0, 0, 0, 0, 1, 1, 0, 0]
+        for k, ci in enumerate(seq):
+            a = off.render(cams[ci], W, H, cfg.depth, rgba32f=True, rgba8=True)
+            b = on.render(cams[ci], W, H, cfg.depth, rgba32f=True, rgba8=True)
+            torch.cuda.synchronize()
+            assert torch.equal(a["rgba32f"], b["rgba32f"]) and torch.equal(a["rgba8"], b["rgba8"]), f"frame {k}"
+    finally:
+        off.close()
+        on.close()
