@@ -755,7 +755,12 @@ __device__ __forceinline__ int closest_hit(const SceneView& V, const Ray& r, d3*
         }
         k0 = 64;
     }
-    for (; k0 < V.np; k0 += kChunk) sphere_batch_closest(V, r, k0, eps, &kind, &best, hp, skip - 1);
+    for (; k0 < V.np; k0 += kChunk) {
+        // (a batch none of whose spheres the mask keeps is missed by every ray of the wave: the cached masks of the
+        // fast kernels, LevelMasks; ~0 otherwise)
+        if (k0 < 64 && ((mask >> k0) & ((1ull << kChunk) - 1)) == 0) continue;
+        sphere_batch_closest(V, r, k0, eps, &kind, &best, hp, skip - 1);
+    }
     if (FULL) meshes_closest(V, r, eps, &kind, &best, hp);
     return kind;
 }
@@ -1115,6 +1120,7 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
         k0 = 64;
     }
     for (; k0 < V.np; k0 += kChunk) {
+        if (k0 < 64 && ((mask >> k0) & ((1ull << kChunk) - 1)) == 0) continue;   // (cached masks, as closest_hit)
         uint32_t pass = 0;
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
@@ -1283,9 +1289,10 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
         set_dir(&sr, sd, sdir);
         const double kd = fabs(dot(n, sdir));               // before the shadow test: fewer live registers
         uint64_t m = ~0ull;
-        if (CULL && !FULL && V.np >= kConeMin) {
-            // (light i's shadow mask at this level: cached per tile for a calibrated static view, LevelMasks)
-            const int t = lm ? lm->tile : -1;
+        const int t = lm ? lm->tile : -1;
+        if (CULL && !FULL && (V.np >= kConeMin || t >= 0)) {
+            // (light i's shadow mask at this level: cached per tile for a calibrated static view, LevelMasks; also
+            // computed for a fast scene when this render writes the cache)
             const uint64_t* in = t >= 0 ? level_masks_in() : nullptr;
             if (in) {
                 m = in[t + lslot + i];
@@ -1294,6 +1301,10 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
                 uint64_t* out = t >= 0 ? level_masks_out() : nullptr;
                 if (out && __lane_id() == 0) out[t + lslot + i] = m;
             }
+        } else if (!CULL && !FULL && t >= 0) {
+            // fast kernels: the cached mask lets occluded skip the filter batches no ray of the wave can meet
+            const uint64_t* in = level_masks_in();
+            if (in) m = in[t + lslot + i];
         }
         bool lit = false;
         if (hit) lit = !(FULL ? occluded_transparent(V, sr) : occluded<false, CULL>(V, sr, i, m, skip));
@@ -1429,7 +1440,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     RT_COUNT(V.S, kCntLevels, 1);
     if (!first) {
         set_origin_f32(V.S, r);
-        if (V.np >= kConeMin) {
+        if (V.np >= kConeMin || lm.tile >= 0) {
             const uint64_t* in = lm.tile >= 0 ? level_masks_in() : nullptr;
             if (in) {
                 smask = in[lm.tile + lvl - 1];              // this tile's level-lvl ray mask (calibrated view)
@@ -1543,7 +1554,12 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t c
                     kind = closest_hit_primary<TRANSP>(V, r, cone, &p, lazy_u);
                 } else {
                     set_origin_f32(S, &r);
-                    kind = closest_hit<TRANSP>(V, r, &p, ~0ull, TRANSP ? -1 : skip, lvl > 0);
+                    uint64_t rm = ~0ull;                    // this tile's cached level-lvl ray mask (LevelMasks)
+                    if (!TRANSP && lm.tile >= 0) {
+                        const uint64_t* in = level_masks_in();
+                        if (in) rm = in[lm.tile + lvl - 1];
+                    }
+                    kind = closest_hit<TRANSP>(V, r, &p, rm, TRANSP ? -1 : skip, lvl > 0);
                 }
             }
             const bool hit = kind >= 0;
@@ -1584,7 +1600,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t c
                     ndsl[2 * SS] = nd.z;
                     asm volatile("" ::: "memory");          // keep it in LDS across the light loop
                 }
-                const d3 c = shade<TRANSP, false, kAcc, SS, ACHRO>(V, true, p, n, mat, ks, skip, psl);
+                const d3 c = shade<TRANSP, false, kAcc, SS, ACHRO>(V, true, p, n, mat, ks, skip, psl, &lm, B + lvl * V.nl);
                 if ((kPark || RT_PARK_NU) && lvl < B) {
                     asm volatile("" ::: "memory");
                     nd = mk(ndsl[0], ndsl[SS], ndsl[2 * SS]);

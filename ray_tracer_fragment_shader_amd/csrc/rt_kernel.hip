@@ -897,9 +897,13 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
     const bool capturing = cap != hipStreamCaptureStatusNone;
     if (capturing) c->ever_captured = true;
     bool calibrate = false, cone_calib = false, lm_calib = false;
-    // level masks per tile (culling kernels of opaque scenes, one-wave tiles): B ray masks + (B + 1) nl shadow masks
-    const bool cull_kernel = c->n_padded >= kConeMin && !c->tree && !c->transparent && !big && RT_WG_FAST == 64;
-    int lm_stride = cull_kernel && c->level_masks && c->cone_cache ? depth + (depth + 1) * c->n_lights : 0;
+    // level masks per tile (opaque scenes, one-wave tiles): B ray masks + (B + 1) nl shadow masks.  The culling
+    // kernels compute them in their calibration render; for the fast kernels' scenes (< kConeMin spheres) a culling
+    // kernel writes them in a launch of its own right after the calibration render (no image outputs), and later
+    // renders skip the filter batches they rule out
+    const bool opaque_tiles = !c->tree && !c->transparent && !big && RT_WG_FAST == 64;
+    const bool cull_kernel = c->n_padded >= kConeMin && opaque_tiles;
+    int lm_stride = opaque_tiles && c->level_masks && c->cone_cache ? depth + (depth + 1) * c->n_lights : 0;
     if (lm_stride > kLevelMaskSlotsMax) lm_stride = 0;
     rt_ctx::ViewKey key{};
     // (dispatch records pack the tile as ty << 16 | tx)
@@ -987,8 +991,10 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
                 (void)hipGetLastError();                // out of memory: the masks stay in the kernel
         }
         if (lm_calib && c->d_lmask) {
-            P.lmask_out = c->d_lmask;
-            P.lmask_stride = lm_stride;
+            if (cull_kernel) {                          // (fast scenes: the mask launch below writes them)
+                P.lmask_out = c->d_lmask;
+                P.lmask_stride = lm_stride;
+            }
         } else {
             lm_calib = false;
         }
@@ -1053,6 +1059,34 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
         default: e = launch_render<7>(L); break;
     }
     if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("rt_render_kernel launch: ") + hipGetErrorString(e));
+    if (lm_calib && !cull_kernel) {
+        // a fast kernel's scene: the level masks of the view from a culling kernel that stores nothing else (identity
+        // order, its own primary cone masks, no image) — stream-ordered before the renders that read them
+        RenderLaunch M = L;
+        M.P.lmask_out = c->d_lmask;
+        M.P.lmask_in = nullptr;
+        M.P.lmask_stride = lm_stride;
+        M.P.disp = nullptr;
+        M.P.cone_use = 0;
+        M.P.cone_out = nullptr;
+        M.P.tile_cost = nullptr;
+        M.o32 = M.o8 = nullptr;
+        M.o64 = nullptr;
+        M.orc = nullptr;
+        M.variant = mw5 ? kVarCull : kVarCullAnyW;
+        M.lds = slot_bytes(depth, false, RT_WG_FAST, true);
+        switch (depth) {
+            case 0: e = launch_render<0>(M); break;
+            case 1: e = launch_render<1>(M); break;
+            case 2: e = launch_render<2>(M); break;
+            case 3: e = launch_render<3>(M); break;
+            case 4: e = launch_render<4>(M); break;
+            case 5: e = launch_render<5>(M); break;
+            case 6: e = launch_render<6>(M); break;
+            default: e = launch_render<7>(M); break;
+        }
+        if (e != hipSuccess) return rt_fail(RT_EHIP, std::string("level-mask launch: ") + hipGetErrorString(e));
+    }
     if (calibrate) {
         // the dispatch table of this view (stream-ordered after the calibration render, which wrote the tile times)
         const dim3 tg((unsigned)((tiles + 255) / 256));

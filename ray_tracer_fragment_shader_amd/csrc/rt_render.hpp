@@ -414,7 +414,7 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
 #endif
     d3 col;
     LevelMasks lm{-1};
-    if (CULL && RT_LEVEL_MASKS && P.lmask_stride > 0 && !pad) lm.tile = (ty * P.tiles_x + tx) * P.lmask_stride;
+    if (RT_LEVEL_MASKS && !TRANSP && !TREE && P.lmask_stride > 0 && !pad) lm.tile = (ty * P.tiles_x + tx) * P.lmask_stride;
     if constexpr (TREE)
         col = trace_tree<B>(V, eye, sp, &seg, &sh);
     else
@@ -531,8 +531,11 @@ void rt_render_kernel_sg(const DispRec* __restrict__ disp, int32_t tiles_x, int3
 #ifndef RT_SG8_B
 #define RT_SG8_B 2
 #endif
+#ifndef RT_SG8_MINW
+#define RT_SG8_MINW 8                          // r06: the 8-wave kernel asks for 8 waves (<= 64 VGPRs) explicitly
+#endif
 template <int B, int MINW, bool CULL, bool PACKED, bool ACHRO = true>
-__global__ __launch_bounds__(RT_WG_FAST, MINW) __attribute__((amdgpu_num_sgpr(RT_FAST8_SGPRS)))
+__global__ __launch_bounds__(RT_WG_FAST, (RT_SG8_MINW > MINW ? RT_SG8_MINW : MINW)) __attribute__((amdgpu_num_sgpr(RT_FAST8_SGPRS)))
 void rt_render_kernel_sg8(const DispRec* __restrict__ disp, int32_t tiles_x, int32_t n_disp,
                           const DevScene* __restrict__ gscene, RenderParams P, void* out32, void* out8, double* out64,
                           uint32_t* outrc) {

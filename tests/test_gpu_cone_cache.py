@@ -181,13 +181,16 @@ def _random_cull_scene(rng, n_spheres, n_lights):
 
 
 @pytest.mark.parametrize("seed,n_spheres,n_lights,depth", [(0, 20, 1, 2), (1, 40, 2, 3), (2, 64, 3, 5),
-                                                           (3, 33, 2, 7), (4, 48, 4, 5)])
+                                                           (3, 33, 2, 7), (4, 48, 4, 5), (5, 8, 1, 1), (6, 12, 2, 2),
+                                                           (7, 9, 3, 4), (8, 6, 2, 3), (9, 3, 1, 2)])
 def test_level_mask_cache_random_culling_scenes(seed, n_spheres, n_lights, depth):
-    """The culling kernels' per-tile level masks (rt_device.hpp LevelMasks): the calibration render of a static view
-    stores every level's ray and shadow masks, later renders of that view read them instead of computing them.  Random
-    scenes of >= 16 spheres (the culling kernels), 1-4 lights, depth 2-7 — including slot counts past the cache's
-    limit (seed 3: 7 + 8 x 2 = 23 slots, cached; seed 4: 5 + 6 x 4 = 29, computed): the first, calibration and cached
-    renders, and a context with the cache off (RT_LEVEL_MASKS=0), all equal the oracle bit for bit."""
+    """Per-tile level masks (rt_device.hpp LevelMasks): the calibration of a static view stores every level's ray and
+    shadow masks — the culling kernels (>= 16 spheres) in the calibration render itself, the fast kernels' scenes
+    (8-15 padded spheres) through a culling launch of its own — and later renders of that view read them (the fast
+    kernels skip the filter batches they rule out).  Random scenes, 1-4 lights, depth 1-7, including slot counts past
+    the cache's limit (seed 3: 7 + 8 x 2 = 23 slots, cached; seed 4: 5 + 6 x 4 = 29, computed) and a scene below the
+    primary cone's 8 spheres (seed 9: no masks): the first, calibration and cached renders equal the oracle bit for
+    bit."""
     rng = np.random.default_rng(seed)
     sc = _random_cull_scene(rng, n_spheres, n_lights)
     W, H = 160, 120

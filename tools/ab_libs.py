@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """In-process, interleaved A/B of library builds: the in-tree lib/librt_amd.so ("base") and every
-tools/_var/<name>/librt_amd.so, each loaded as its own handle (copied to a private path) in ONE process, with
+tools/_ab/<name>/librt_amd.so (r06: the experiment builds that travel to the GPU box; tools/_var stays local), each loaded as its own handle (copied to a private path) in ONE process, with
 their renders interleaved round by round — so box-to-box and process-to-process clock differences (±2% at c2)
 cancel out.
 
@@ -45,7 +45,7 @@ def main():
     tmp = tempfile.mkdtemp()
     libs = {"base": load(abi.LIB_PATH, tmp, "base")}
     only = set(os.environ["VARS"].split(",")) if os.environ.get("VARS") else None
-    for d in sorted(glob.glob(os.path.join(ROOT, "tools", "_var", "*", "librt_amd.so"))):
+    for d in sorted(glob.glob(os.path.join(ROOT, "tools", os.environ.get("AB_DIR", "_ab"), "*", "librt_amd.so"))):
         name = os.path.basename(os.path.dirname(d))
         if only is None or name in only:
             libs[name] = load(d, tmp, name)
