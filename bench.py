@@ -335,6 +335,7 @@ def c4_scaling_keys(n, W, H, rays, c4_ms, c3_ms_inflight, c3_ms_serial):
     return out
 
 
+GROUP_BUFFERS = 3                                      # rt_group.cpp kBufs: frame buffers per rank
 XGMI_LINK_GBS = 153.0                                   # nominal per-link rate (7 links per MI355X); not measured here
 
 
@@ -443,31 +444,33 @@ def c4_rank_projection(torch, L, abi, Tracer, cfg, dev, local, n, band_height, c
     e[1].record(sts[0])
     torch.cuda.synchronize()
     unpack_ms = e[0].elapsed_time(e[1]) / 40
-    # rank 0 as rt_render_multi runs it: bands on the two render streams in turn, each frame's unpack (its slab and the
-    # gathered peers' bands, pre-filled) on a high-priority comm stream behind that frame's render
+    # rank 0 as rt_render_multi runs it: bands on the two render streams in turn into three frame buffers, each frame's
+    # unpack (its slab and the gathered peers' bands, pre-filled) on the comm stream (default priority, as the group)
+    # behind that frame's render
     t = Tracer(local)
     t.set_scene(cfg.scene())
     rows = abi.rt_rows(hb, n, 0, 1)
-    gath = [torch.zeros((n * sr, W), dtype=torch.uint8, device=dev) for _ in range(2)]
-    cs = torch.cuda.Stream(dev, priority=-1)
-    ev_r = [torch.cuda.Event() for _ in range(2)]
-    ev_a = [torch.cuda.Event() for _ in range(2)]
+    nb = GROUP_BUFFERS
+    gath = [torch.zeros((n * sr, W), dtype=torch.uint8, device=dev) for _ in range(nb)]
+    cs = torch.cuda.Stream(dev)
+    ev_r = [torch.cuda.Event() for _ in range(nb)]
+    ev_a = [torch.cuda.Event() for _ in range(nb)]
     la = [(t._ctx, ctypes.byref(cam), W, H, B, ctypes.byref(rows), abi.RT_PIXEL_GRAY32F, None, abi.RT_PIXEL_GRAY8,
-           ctypes.c_void_p(gath[k].data_ptr()), ctypes.c_void_p(sts[k].cuda_stream)) for k in range(2)]
-    ub = [(ctypes.c_void_p(gath[k].data_ptr()), ctypes.c_void_p(img.data_ptr()), W, H, abi.RT_PIXEL_GRAY8,
-           abi.RT_PIXEL_RGBA8, hb, n, sr, ctypes.c_void_p(cs.cuda_stream)) for k in range(2)]
-    used = [False, False]
+           ctypes.c_void_p(gath[b].data_ptr())) for b in range(nb)]
+    ub = [(ctypes.c_void_p(gath[b].data_ptr()), ctypes.c_void_p(img.data_ptr()), W, H, abi.RT_PIXEL_GRAY8,
+           abi.RT_PIXEL_RGBA8, hb, n, sr, ctypes.c_void_p(cs.cuda_stream)) for b in range(nb)]
+    used = [False] * nb
 
     def root_frame(f):
-        k = f & 1
-        if used[k]:
-            sts[k].wait_event(ev_a[k])                        # frame f - 2's unpack has read slab k
-        abi.check(L.rt_render_dev_packed(*la[k]), "rt_render_dev_packed")
-        ev_r[k].record(sts[k])
-        cs.wait_event(ev_r[k])
-        abi.check(L.rt_unpack_dev(*ub[k]), "rt_unpack_dev")
-        ev_a[k].record(cs)
-        used[k] = True
+        b, k = f % nb, f & 1
+        if used[b]:
+            sts[k].wait_event(ev_a[b])                        # frame f - nb's unpack has read buffer b
+        abi.check(L.rt_render_dev_packed(*la[b], ctypes.c_void_p(sts[k].cuda_stream)), "rt_render_dev_packed")
+        ev_r[b].record(sts[k])
+        cs.wait_event(ev_r[b])
+        abi.check(L.rt_unpack_dev(*ub[b]), "rt_unpack_dev")
+        ev_a[b].record(cs)
+        used[b] = True
     for f in range(3 + frames // 2):
         root_frame(f)
     torch.cuda.synchronize()

@@ -16,7 +16,7 @@
 //                        -> record assembled[b]; the caller's stream waits for assembled[b]
 // A process's ranks must switch scenes between the same frames: one-process-per-GPU groups agree on the scene
 // (hence the wire formats) with a small all-reduce whenever a rank's scene changes (agree_on_scene).
-// Stream priorities: rs[0], rs[1] lowest, cs highest (the gather's kernels do not queue behind the next render grid).
+// Stream priorities: all at the device's default (a high-priority comm stream preempts the renders, setup_rank).
 // A one-rank group renders straight into the caller's image on the caller's stream (identity band plan).
 //
 // What travels: the wire formats.  An achromatic scene (every colour term with R = G = B, rt_scene_achromatic)
@@ -25,8 +25,8 @@
 // in the same kernel that puts the bands in image order (rt_unpack_dev).  At c4 (3840 x 2160 over 8 ranks) the
 // root's ingress is 7/8 of 8.3 MB instead of 7/8 of 33.2 MB.
 //
-// b = frame & 1: the slabs and the root's gather buffer are double-buffered, so frame f's gather overlaps
-// frame f+1's render.  Transports: RCCL (ncclCommInitAll for one process driving n GPUs, ncclCommInitRank
+// b = frame % n_bufs (3): the slabs and the root's gather buffer are triple-buffered, so frame f's gather overlaps
+// the renders of frames f+1 and f+2.  Transports: RCCL (ncclCommInitAll for one process driving n GPUs, ncclCommInitRank
 // for one process per GPU) or COPY (hipMemcpyPeerAsync on the root's comm stream; used when contexts share
 // a device — RCCL refuses two ranks on one GPU — which is how the n-rank logic is exercised on one GPU).
 #include <hip/hip_runtime.h>
@@ -47,6 +47,15 @@ namespace {
 constexpr int kKinds = 2;                      // 0: the RGBA32F image, 1: the RGBA8 image
 constexpr int kImageFormat[kKinds] = {RT_PIXEL_RGBA32F, RT_PIXEL_RGBA8};
 constexpr int kRing = 64;                      // frames of per-phase timing events kept
+// Frame buffers (slabs, the root's gather buffer and their events): frame f uses buffer f % n_bufs.  A buffer is
+// rendered into again only once frame f - n_bufs has left it (its send, the root's unpack): with two, a rank's render of
+// frame f + 2 waits for frame f's send / unpack, which waits for frame f's render — a chain of one render and one
+// exchange per two frames; a third buffer lets it run a frame further ahead (rank 0's pipeline at 8 ranks, one GPU:
+// 41 -> 30 us per frame when its streams have hardware queues of their own, tools/c4_gap_probe.py part 6).  RCCL groups
+// (one device per rank) use 3; COPY groups (every rank on one device: 3 streams per rank oversubscribe its hardware
+// queues, and with 3 buffers the frame time jumped between 0.20 and 1.06 ms run to run, tools/c4_copy_probe.py) use 2.
+// RT_GROUP_BUFFERS=2|3 overrides.
+constexpr int kBufs = 3;
 
 // Per-phase timing events of one frame on one rank (rt_group_timing): render start / end on the render stream,
 // gather start (the rank's render is done) / end on the comm stream, and on the root the assembled image.
@@ -66,11 +75,11 @@ struct Rank {
     // render may still read, which the context would otherwise resolve with a device synchronisation).
     hipStream_t rs[2] = {nullptr, nullptr}, cs = nullptr;
     int last_rs = 1;                           // rs index of the previous frame
-    hipEvent_t rendered[2] = {nullptr, nullptr};
-    hipEvent_t sent[2] = {nullptr, nullptr};   // on cs (RCCL) or on the root's comm stream (COPY)
-    bool sent_rec[2] = {false, false};
-    void* slab[2][kKinds] = {{nullptr, nullptr}, {nullptr, nullptr}};
-    size_t slab_cap[2][kKinds] = {{0, 0}, {0, 0}};
+    hipEvent_t rendered[kBufs] = {};
+    hipEvent_t sent[kBufs] = {};               // on cs (RCCL) or on the root's comm stream (COPY)
+    bool sent_rec[kBufs] = {};
+    void* slab[kBufs][kKinds] = {};
+    size_t slab_cap[kBufs][kKinds] = {};
     ncclComm_t comm = nullptr;
     uint64_t* d_agree = nullptr;               // rt_group_create_rank: the scene agreement's all-reduce buffer
     uint64_t agreed_fp = 0;                    // the scene fingerprint the group last agreed on
@@ -86,11 +95,12 @@ struct rt_group {
     bool owns_root = false;                    // rank 0 is one of this process's ranks (ranks[0])
     std::vector<Rank> ranks;                   // this process's ranks
     // root only
-    void* gathered[2][kKinds] = {{nullptr, nullptr}, {nullptr, nullptr}};
-    size_t gathered_cap[2][kKinds] = {{0, 0}, {0, 0}};
-    hipEvent_t received[2] = {nullptr, nullptr};
-    hipEvent_t assembled[2] = {nullptr, nullptr};
-    bool assembled_rec[2] = {false, false};
+    void* gathered[kBufs][kKinds] = {};
+    size_t gathered_cap[kBufs][kKinds] = {};
+    hipEvent_t received[kBufs] = {};
+    hipEvent_t assembled[kBufs] = {};
+    bool assembled_rec[kBufs] = {};
+    int n_bufs = kBufs;                        // RT_GROUP_BUFFERS (A/B): 2
     uint64_t frame = 0;
     int last_band = 0, last_slab_rows = 0;
     // timing (rt_group_timing): frames [t_first, frame) are recorded, the last kRing of them kept
@@ -136,19 +146,27 @@ int grow(void** p, size_t* cap, size_t bytes) {
     return RT_OK;
 }
 
+bool comm_high_priority() {
+    const char* e = getenv("RT_GROUP_COMM_PRIORITY");
+    return e && atoi(e) == 1;
+}
+
 int setup_rank(Rank* r, rt_ctx* ctx, int rank, hipEvent_t* sent_device_events) {
     r->ctx = ctx;
     r->rank = rank;
     r->device = rt_ctx_device(ctx);
     G_HIP(hipSetDevice(r->device));
-    // The render stream gets the lowest priority and the comm stream (RCCL send/recv, and on the root the
-    // unshuffle) the highest: a frame's gather kernels are dispatched as soon as CUs free up instead of
-    // queueing behind the next frame's render grid, so the exchange overlaps the render.
+    // Every stream at the device's lowest (default) priority.  r02-r05 gave the comm stream (RCCL send/recv, the
+    // root's unpack) the greatest priority so its kernels would not queue behind the next render grid; measured on
+    // MI355X (tools/c4_gap_probe.py part 6, rank 0's pipeline at 8 ranks: bands on two streams, each frame's unpack on
+    // the comm stream), a high-priority comm stream runs 120 us per frame against 39 us at normal priority — the
+    // renders on the other queues are preempted around every high-priority dispatch.  RT_GROUP_COMM_PRIORITY=1 (A/B)
+    // restores it.
     int least = 0, greatest = 0;
     G_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
     for (int k = 0; k < 2; ++k) G_HIP(hipStreamCreateWithPriority(&r->rs[k], hipStreamNonBlocking, least));
-    G_HIP(hipStreamCreateWithPriority(&r->cs, hipStreamNonBlocking, greatest));
-    for (int b = 0; b < 2; ++b) {
+    G_HIP(hipStreamCreateWithPriority(&r->cs, hipStreamNonBlocking, comm_high_priority() ? greatest : least));
+    for (int b = 0; b < kBufs; ++b) {
         G_HIP(hipEventCreateWithFlags(&r->rendered[b], hipEventDisableTiming));
         if (!sent_device_events) G_HIP(hipEventCreateWithFlags(&r->sent[b], hipEventDisableTiming));
         else r->sent[b] = sent_device_events[b];
@@ -158,7 +176,7 @@ int setup_rank(Rank* r, rt_ctx* ctx, int rank, hipEvent_t* sent_device_events) {
 
 int setup_root_events(rt_group* g) {
     G_HIP(hipSetDevice(g->ranks[0].device));
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < kBufs; ++b) {
         G_HIP(hipEventCreateWithFlags(&g->received[b], hipEventDisableTiming));
         G_HIP(hipEventCreateWithFlags(&g->assembled[b], hipEventDisableTiming));
     }
@@ -191,7 +209,7 @@ extern "C" int rt_group_destroy(rt_group* g) {
         for (auto& e : r.ph)
             for (hipEvent_t ev : {e.r0, e.r1, e.g0, e.g1, e.a1})
                 if (ev) (void)hipEventDestroy(ev);
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < kBufs; ++b) {
             if (r.rendered[b]) (void)hipEventDestroy(r.rendered[b]);
             if (r.sent[b] && g->transport == RT_TRANSPORT_RCCL) (void)hipEventDestroy(r.sent[b]);
             for (int k = 0; k < kKinds; ++k)
@@ -203,7 +221,7 @@ extern "C" int rt_group_destroy(rt_group* g) {
     }
     if (g->owns_root && !g->ranks.empty()) {
         (void)hipSetDevice(g->ranks[0].device);
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < kBufs; ++b) {
             if (g->received[b]) (void)hipEventDestroy(g->received[b]);
             if (g->assembled[b]) (void)hipEventDestroy(g->assembled[b]);
             for (int k = 0; k < kKinds; ++k)
@@ -211,7 +229,7 @@ extern "C" int rt_group_destroy(rt_group* g) {
         }
         if (g->transport == RT_TRANSPORT_COPY)          // COPY: every rank's `sent` events live on the root
             for (auto& r : g->ranks)
-                for (int b = 0; b < 2; ++b)
+                for (int b = 0; b < kBufs; ++b)
                     if (r.sent[b]) (void)hipEventDestroy(r.sent[b]);
     }
     delete g;
@@ -240,25 +258,27 @@ extern "C" int rt_group_create(rt_ctx* const* ctxs, int n, int transport, rt_gro
     rt_group* g = new rt_group();
     if (const char* e = getenv("RT_GATHER_ROOT_WAITS")) g->root_waits = atoi(e) != 0;
     if (const char* e = getenv("RT_GROUP_RENDER_STREAMS")) g->render_streams = atoi(e) == 1 ? 1 : 2;
+    if (const char* e = getenv("RT_GROUP_BUFFERS")) g->n_bufs = atoi(e) == 2 ? 2 : kBufs;
     g->n_ranks = n;
     g->transport = transport;
+    if (transport == RT_TRANSPORT_COPY && !getenv("RT_GROUP_BUFFERS")) g->n_bufs = 2;
     g->owns_root = true;
     g->ranks.resize(n);
     g->plan.resize(n);
     int rc = RT_OK;
     // COPY: the root's comm stream records every rank's `sent` events, so they live on the root device.
-    std::vector<hipEvent_t> root_sent(2 * n, nullptr);
+    std::vector<hipEvent_t> root_sent(kBufs * n, nullptr);
     if (transport == RT_TRANSPORT_COPY) {
         if (hipSetDevice(devs[0]) != hipSuccess) { delete g; return rt_fail(RT_EHIP, "rt_group_create: hipSetDevice"); }
         for (int q = 0; q < n; ++q)
-            for (int b = 0; b < 2; ++b) {
-                if (hipEventCreateWithFlags(&root_sent[2 * q + b], hipEventDisableTiming) != hipSuccess)
+            for (int b = 0; b < kBufs; ++b) {
+                if (hipEventCreateWithFlags(&root_sent[kBufs * q + b], hipEventDisableTiming) != hipSuccess)
                     rc = rt_fail(RT_EHIP, "rt_group_create: hipEventCreate failed");
-                g->ranks[q].sent[b] = root_sent[2 * q + b];    // owned by the group from here on
+                g->ranks[q].sent[b] = root_sent[kBufs * q + b];    // owned by the group from here on
             }
     }
     for (int q = 0; q < n && rc == RT_OK; ++q)
-        rc = setup_rank(&g->ranks[q], ctxs[q], q, transport == RT_TRANSPORT_COPY ? &root_sent[2 * q] : nullptr);
+        rc = setup_rank(&g->ranks[q], ctxs[q], q, transport == RT_TRANSPORT_COPY ? &root_sent[kBufs * q] : nullptr);
     if (rc == RT_OK) rc = setup_root_events(g);
     if (rc == RT_OK && transport == RT_TRANSPORT_RCCL) {
         std::vector<ncclComm_t> comms(n);
@@ -283,6 +303,7 @@ extern "C" int rt_group_create_rank(rt_ctx* ctx, int n_ranks, int rank, const ui
     rt_group* g = new rt_group();
     if (const char* e = getenv("RT_GATHER_ROOT_WAITS")) g->root_waits = atoi(e) != 0;
     if (const char* e = getenv("RT_GROUP_RENDER_STREAMS")) g->render_streams = atoi(e) == 1 ? 1 : 2;
+    if (const char* e = getenv("RT_GROUP_BUFFERS")) g->n_bufs = atoi(e) == 2 ? 2 : kBufs;
     g->n_ranks = n_ranks;
     g->transport = RT_TRANSPORT_RCCL;
     g->owns_root = rank == 0;
@@ -434,7 +455,7 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     if (g->owns_root && ((kind_on[0] && !rgba32f) || (kind_on[1] && !rgba8)))
         return rt_fail(RT_EINVAL, "rt_render_multi: rank 0 needs a device image for every requested output");
     int rc = RT_OK;
-    const int b = (int)(g->frame & 1);
+    const int b = (int)(g->frame % (uint64_t)g->n_bufs);
     const int slot = (int)(g->frame % kRing);
     const hipStream_t st = (hipStream_t)stream;
     // Every local rank must hold the same scene: the frame is assembled from their bands, and the wire formats are
@@ -497,7 +518,7 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         return RT_OK;
     }
 
-    // ---- buffers (grow-only).  A buffer that must grow may still be in use by frame - 2 (a peer copy or an RCCL
+    // ---- buffers (grow-only).  A buffer that must grow may still be in use by frame - n_bufs (a peer copy or an RCCL
     // receive on the root, a send on a rank, the root's unshuffle): wait for the group and the caller's stream
     // first, whatever changed (width, band plan, outputs, wire format). ----
     bool must_grow = false;
@@ -549,9 +570,9 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         const hipStream_t rs = r.rs[k];
         r.last_rs = k;
         G_HIP(hipSetDevice(r.device));
-        if (r.sent_rec[b]) G_HIP(hipStreamWaitEvent(rs, r.sent[b], 0));       // slab[b] has left (frame - 2)
+        if (r.sent_rec[b]) G_HIP(hipStreamWaitEvent(rs, r.sent[b], 0));       // slab[b] has left (frame - n_bufs)
         if (r.rank == 0 && g->assembled_rec[b])                               // the root's slab[b] is read by
-            G_HIP(hipStreamWaitEvent(rs, g->assembled[b], 0));                // frame - 2's unshuffle
+            G_HIP(hipStreamWaitEvent(rs, g->assembled[b], 0));                // frame - n_bufs's unshuffle
         if (pe[q]) G_HIP(hipEventRecord(pe[q]->r0, rs));
         rt_rows rows = {hb, g->n_ranks, r.rank, 1};
         rc = rt_render_dev_packed(r.ctx, cam, W, H, depth, &rows, wire[0], kind_on[0] ? r.slab[b][0] : nullptr,

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """rt_render_multi on one GPU with n COPY-transport ranks (c3's 3840x2160 frame, GRAY8 wire): per-phase times
-from rt_group_get_stats and the per-frame wall time, with the root's gather posted at once (default) and, for
-A/B, waiting for the root's own render first (RT_GATHER_ROOT_WAITS=1, the r03 ordering).  Frames are checked
-byte for byte against a one-launch render."""
+from rt_group_get_stats and the per-frame wall time, for each setting of an A/B environment variable (AB_VAR, default
+RT_GROUP_COMM_PRIORITY: the comm streams at the default or the greatest priority; RT_GATHER_ROOT_WAITS: the root's
+gather posted at once or after its own render).  Frames are checked byte for byte against a one-launch render."""
 import ctypes
 import json
 import os
@@ -28,8 +28,8 @@ torch.cuda.synchronize()
 out = {}
 for rnd in range(int(os.environ.get("ROUNDS", "3"))):
     for n in (2, 4, 8):
-        for waits in ("0", "1"):
-            os.environ["RT_GATHER_ROOT_WAITS"] = waits
+        for waits in os.environ.get("AB_VALUES", "0,1").split(","):
+            os.environ[os.environ.get("AB_VAR", "RT_GROUP_COMM_PRIORITY")] = waits
             ctxs = [Tracer(0) for _ in range(n)]
             for c in ctxs:
                 c.set_scene(sc)
@@ -37,7 +37,7 @@ for rnd in range(int(os.environ.get("ROUNDS", "3"))):
             g = ctypes.c_void_p()
             abi.check(L.rt_group_create(arr, n, abi.RT_TRANSPORT_COPY, ctypes.byref(g)), "rt_group_create")
             img = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
-            st = torch.cuda.current_stream()
+            st = torch.cuda.Stream()
             argv = (g, ctypes.byref(cam), W, H, B, 0, abi.RT_OUT_RGBA8, None, ctypes.c_void_p(img.data_ptr()),
                     ctypes.c_void_p(st.cuda_stream))
             for _ in range(12):
@@ -59,7 +59,7 @@ for rnd in range(int(os.environ.get("ROUNDS", "3"))):
             abi.check(L.rt_group_get_stats(g, ctypes.byref(s)), "stats")
             torch.cuda.synchronize()
             assert torch.equal(img, want), (n, waits)
-            key = f"n{n}_root_waits{waits}"
+            key = f"n{n}_{os.environ.get('AB_VAR', 'RT_GROUP_COMM_PRIORITY')}={waits}"
             out.setdefault(key, []).append({"wall_ms": round(wall, 4), "render_ms": round(s.render_ms, 4),
                                             "gather_ms": round(s.gather_ms, 4), "assemble_ms": round(s.assemble_ms, 4),
                                             "frame_ms": round(s.frame_ms, 4)})

@@ -305,6 +305,59 @@ def part5():
             tt.close()
 
 
+def part6():
+    """Rank 0's pipeline at n = 8 (band height 8) as rt_render_multi runs it — its bands on two render streams in turn
+    into NB frame buffers, each frame's unpack on the comm stream behind that frame's render, a buffer rendered into
+    again once its unpack is done — for NB = 2, 3 and the comm stream at normal and high priority (r02-r05's group
+    used the greatest), and the bands alone."""
+    n = 8
+    band, slab = ctypes.c_int(), ctypes.c_int()
+    abi.check(L.rt_band_plan(H, n, 8, ctypes.byref(band), ctypes.byref(slab)), "rt_band_plan")
+    hb, sr = band.value, slab.value
+    img = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+    for nb, prio, unpack in ((3, 0, True), (4, 0, True), (6, 0, True), (4, 0, "decoupled"), (4, 0, False)):
+        t = Tracer(0)
+        t.set_scene(cfg.scene())
+        rows = abi.rt_rows(hb, n, 0, 1)
+        sts = [torch.cuda.Stream() for _ in range(2)]
+        cs = torch.cuda.Stream(priority=prio)
+        gath = [torch.zeros((n * sr, W), dtype=torch.uint8, device="cuda") for _ in range(nb)]
+        ev_r = [torch.cuda.Event() for _ in range(nb)]
+        ev_a = [torch.cuda.Event() for _ in range(nb)]
+        used = [False] * nb
+
+        def frame(f, nb=nb, unpack=unpack, sts=sts, cs=cs, gath=gath, ev_r=ev_r, ev_a=ev_a, used=used, t=t, rows=rows):
+            b, k = f % nb, f & 1
+            if used[b] and unpack != "decoupled":          # decoupled: the root's bands go straight to the image
+                sts[k].wait_event(ev_a[b])
+            abi.check(L.rt_render_dev_packed(t._ctx, ctypes.byref(cam), W, H, B, ctypes.byref(rows), abi.RT_PIXEL_GRAY32F,
+                                             None, abi.RT_PIXEL_GRAY8, ctypes.c_void_p(gath[b].data_ptr()),
+                                             ctypes.c_void_p(sts[k].cuda_stream)), "render")
+            ev_r[b].record(sts[k])
+            if unpack:
+                if unpack != "decoupled":
+                    cs.wait_event(ev_r[b])
+                abi.check(L.rt_unpack_dev(ctypes.c_void_p(gath[b].data_ptr()), ctypes.c_void_p(img.data_ptr()), W, H,
+                                          abi.RT_PIXEL_GRAY8, abi.RT_PIXEL_RGBA8, hb, n, sr,
+                                          ctypes.c_void_p(cs.cuda_stream)), "unpack")
+            ev_a[b].record(cs if unpack else sts[k])
+            used[b] = True
+        for f in range(6):
+            frame(f)
+        torch.cuda.synchronize()
+        cnt = [0]
+
+        def g(frame=frame, cnt=cnt):
+            cnt[0] += 1
+            frame(cnt[0])
+            return 0
+        settle(g, 0.1)
+        ms = [wall_ms(g, 120, torch.cuda.synchronize) for _ in range(3)]
+        print(json.dumps({"part": 6, "buffers": nb, "comm_priority": prio, "unpack": unpack,
+                          "ms_per_frame": [round(x, 5) for x in ms]}), flush=True)
+        t.close()
+
+
 if __name__ == "__main__":
     parts = os.environ.get("PARTS", "1,2").split(",")
     if "1" in parts:
@@ -317,3 +370,5 @@ if __name__ == "__main__":
         part4()
     if "5" in parts:
         part5()
+    if "6" in parts:
+        part6()
