@@ -243,11 +243,11 @@ def kernel_rooflines(cfg_name, nl, W, H, avg_kern_ms):
              "reference_flops_per_launch": ref_flops})
 
 
-ROCPROF_ONE_STREAM = "profiles/r05/{cfg}_kernel_stats_1stream.csv"
+ROCPROF_ONE_STREAM = "profiles/r06/{cfg}_kernel_stats_1stream.csv"
 
 
 def rocprof_reference(cfg_name, full_frame):
-    """The committed one-stream rocprofv3 --kernel-trace --stats summary of this config (tools/gpu_r05.sh STEPS=prof:
+    """The committed one-stream rocprofv3 --kernel-trace --stats summary of this config (tools/gpu_r06.sh STEPS=prof:
     bench.py --frames-in-flight 1 --profile-kernel-only): AverageNs of rt_render_kernel is the launch duration,
     so bytes / AverageNs / peak reproduces `frac` from profiles/ alone."""
     path = os.path.join(ROOT, ROCPROF_ONE_STREAM.format(cfg=cfg_name))

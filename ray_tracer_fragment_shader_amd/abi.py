@@ -12,7 +12,8 @@ from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_uin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "librt_amd.so")
+# (RT_LIB_PATH: an experiment build of the same ABI, for the instruction-count tools; the product loads LIB_DIR's)
+LIB_PATH = os.environ.get("RT_LIB_PATH") or os.path.join(LIB_DIR, "librt_amd.so")
 
 RT_OK = 0
 RT_EINVAL = -1

@@ -30,6 +30,9 @@
 #ifndef RT_WAVE_TRACE
 #define RT_WAVE_TRACE 0
 #endif
+#ifndef RT_ABLATE
+#define RT_ABLATE 0                            // instruction-count ablation builds (tools/ablate.sh): 1 prologue, 2 no stores
+#endif
 // __launch_bounds__ minimum waves per EU of the depth <= 3 render kernels.  0 (default): 6 for depth <= 2
 // (<= 80 VGPRs, no spills since the bounce loop stopped carrying the previous ray through the light loop),
 // 5 for depth 3 (<= 96 VGPRs; 6 would spill 8 B/lane).
@@ -412,6 +415,11 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
 #if RT_WAVE_TRACE
     const uint64_t t_mid = __builtin_amdgcn_s_memrealtime();   // prologue done: the primary ray is formed
 #endif
+#if RT_ABLATE == 1
+    // (instruction-count ablation builds only, tools/ablate.sh: the prologue alone — no trace, no stores)
+    asm volatile("" ::"v"(sp.x), "v"(sp.y), "v"(sp.z), "s"(cone));
+    return;
+#endif
     d3 col;
     LevelMasks lm{-1};
     if (RT_LEVEL_MASKS && !TRANSP && !TREE && P.lmask_stride > 0 && !pad) lm.tile = (ty * P.tiles_x + tx) * P.lmask_stride;
@@ -422,6 +430,10 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
 #if RT_WAVE_TRACE >= 2
     asm volatile("" ::"v"(col.x), "v"(col.y), "v"(col.z));
     const uint64_t t_trace = __builtin_amdgcn_s_memrealtime();   // trace() done, the stores next
+#endif
+#if RT_ABLATE == 2
+    asm volatile("" ::"v"(col.x), "v"(col.y), "v"(col.z), "v"(seg), "v"(sh));   // (ablation: trace, no stores)
+    return;
 #endif
 
     if (WG != kThreads || !P.wg_staging) {
