@@ -339,7 +339,7 @@ GROUP_BUFFERS = 3                                      # rt_group.cpp kBufs: fra
 XGMI_LINK_GBS = 153.0                                   # nominal per-link rate (7 links per MI355X); not measured here
 
 
-def c4_projection_keys(n, c3_ms_per_frame, rank_ms, unpack_ms, slab_bytes, root_ms=None):
+def c4_projection_keys(n, c3_ms_per_frame, rank_ms, unpack_ms, slab_bytes, root_ms=None, root_renders=True):
     """One GPU's projection of an n-rank c4 frame (rt_render_multi at n ranks cannot run on one GPU): every rank's band
     set rendered alone the way the group renders it (rank_ms[r], per frame, frames in flight as the group keeps them),
     and rank 0's unpack of the n-rank gathered buffer (unpack_ms, alone).  root_ms: rank 0's own pipeline measured as
@@ -347,18 +347,26 @@ def c4_projection_keys(n, c3_ms_per_frame, rank_ms, unpack_ms, slab_bytes, root_
     behind that frame's render — so the unpack overlaps the next render; without it rank 0 is charged its render plus
     the whole unpack.  Projected frame interval = the slowest stage: max(rank_ms[1:], rank 0), or the gather (each
     peer's slab_bytes over its own xGMI link into rank 0, double-buffered behind the next render) at the nominal link
-    rate — not measured — when that is longer."""
+    rate — not measured — when that is longer.  root_renders False (rt_group_root_renders, from 4 ranks): rank_ms are
+    the n - 1 renderers' (ranks 1 .. n - 1) and rank 0 only receives and unpacks (root_ms, or unpack_ms)."""
     render = max(rank_ms)
-    root = root_ms if root_ms is not None else rank_ms[0] + unpack_ms
-    frame = max(max(rank_ms[1:], default=0.0), root)
+    if root_renders:
+        root = root_ms if root_ms is not None else rank_ms[0] + unpack_ms
+        peers = rank_ms[1:]
+    else:
+        root = root_ms if root_ms is not None else unpack_ms
+        peers = rank_ms
+    frame = max(max(peers, default=0.0), root)
     xfer = slab_bytes / (XGMI_LINK_GBS * 1e9) * 1e3
     bound = max(frame, xfer)
     key = f"n{n}"
-    out = {f"{key}_rank_render_ms": [round(x, 5) for x in rank_ms], f"{key}_rank_render_ms_max": round(render, 5),
+    out = {f"{key}_root_renders": bool(root_renders),
+           f"{key}_rank_render_ms": [round(x, 5) for x in rank_ms], f"{key}_rank_render_ms_max": round(render, 5),
            f"{key}_unpack_ms": round(unpack_ms, 5), f"{key}_rank0_ms": round(root, 5),
            f"{key}_projected_frame_ms": round(bound, 5), f"{key}_gather_ms_nominal": round(xfer, 5),
            f"{key}_limiting_stage": ("gather (nominal xGMI)" if xfer > frame else
-                                     "rank 0 (bands + unpack)" if root >= frame else "a peer's band render"),
+                                     ("rank 0 (bands + unpack)" if root_renders else "rank 0 (unpack)")
+                                     if root >= frame else "a peer's band render"),
            f"{key}_speedup_bound": round(c3_ms_per_frame / bound, 3)}
     return out
 
@@ -404,15 +412,16 @@ def c4_rank_projection(torch, L, abi, Tracer, cfg, dev, local, n, band_height, c
     calibration renders; then rank 0's rt_unpack_dev of an n-rank gathered GRAY8 buffer into the RGBA8 image."""
     W, H, B = cfg.width, cfg.height, cfg.depth
     cam = cfg.camera()
-    band, slab = ctypes.c_int(), ctypes.c_int()
-    abi.check(L.rt_band_plan(H, n, band_height, ctypes.byref(band), ctypes.byref(slab)), "rt_band_plan")
-    hb, sr = band.value, slab.value
+    # the group's plan: from 4 ranks rank 0 only assembles and the bands go to ranks 1 .. n - 1 (rt_group_root_renders)
+    plan = abi.rt_group_plan()
+    abi.check(L.rt_group_plan_frame(W, H, n, 0, band_height, abi.RT_OUT_RGBA8, 1, ctypes.byref(plan)), "plan")
+    hb, sr, nr, root_renders = plan.band_height, plan.slab_rows, plan.renderers, bool(plan.root_renders)
     sts = [torch.cuda.Stream(dev) for _ in range(2)]
     rank_ms = []
-    for r in range(n):
+    for r in range(nr):                                      # renderer r (rank r, or r + 1 when rank 0 assembles)
         t = Tracer(local)
         t.set_scene(cfg.scene())
-        rows = abi.rt_rows(hb, n, r, 1)
+        rows = abi.rt_rows(hb, nr, r, 1)
         slabs = [torch.empty((sr, W), dtype=torch.uint8, device=dev) for _ in range(2)]
         la = [(t._ctx, ctypes.byref(cam), W, H, B, ctypes.byref(rows), abi.RT_PIXEL_GRAY32F, None, abi.RT_PIXEL_GRAY8,
                ctypes.c_void_p(slabs[k].data_ptr()), ctypes.c_void_p(sts[k].cuda_stream)) for k in range(2)]
@@ -430,10 +439,10 @@ def c4_rank_projection(torch, L, abi, Tracer, cfg, dev, local, n, band_height, c
         torch.cuda.synchronize()
         rank_ms.append((time.perf_counter() - t0) * 1e3 / frames)
         t.close()
-    gathered = torch.zeros((n * sr, W), dtype=torch.uint8, device=dev)
+    gathered = torch.zeros((nr * sr, W), dtype=torch.uint8, device=dev)
     img = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
     ua = (ctypes.c_void_p(gathered.data_ptr()), ctypes.c_void_p(img.data_ptr()), W, H, abi.RT_PIXEL_GRAY8,
-          abi.RT_PIXEL_RGBA8, hb, n, sr, ctypes.c_void_p(sts[0].cuda_stream))
+          abi.RT_PIXEL_RGBA8, hb, nr, sr, ctypes.c_void_p(sts[0].cuda_stream))
     for _ in range(10):
         abi.check(L.rt_unpack_dev(*ua), "rt_unpack_dev")
     e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -449,25 +458,26 @@ def c4_rank_projection(torch, L, abi, Tracer, cfg, dev, local, n, band_height, c
     # behind that frame's render
     t = Tracer(local)
     t.set_scene(cfg.scene())
-    rows = abi.rt_rows(hb, n, 0, 1)
+    rows = abi.rt_rows(hb, nr, 0, 1)
     nb = GROUP_BUFFERS
-    gath = [torch.zeros((n * sr, W), dtype=torch.uint8, device=dev) for _ in range(nb)]
+    gath = [torch.zeros((nr * sr, W), dtype=torch.uint8, device=dev) for _ in range(nb)]
     cs = torch.cuda.Stream(dev)
     ev_r = [torch.cuda.Event() for _ in range(nb)]
     ev_a = [torch.cuda.Event() for _ in range(nb)]
     la = [(t._ctx, ctypes.byref(cam), W, H, B, ctypes.byref(rows), abi.RT_PIXEL_GRAY32F, None, abi.RT_PIXEL_GRAY8,
            ctypes.c_void_p(gath[b].data_ptr())) for b in range(nb)]
     ub = [(ctypes.c_void_p(gath[b].data_ptr()), ctypes.c_void_p(img.data_ptr()), W, H, abi.RT_PIXEL_GRAY8,
-           abi.RT_PIXEL_RGBA8, hb, n, sr, ctypes.c_void_p(cs.cuda_stream)) for b in range(nb)]
+           abi.RT_PIXEL_RGBA8, hb, nr, sr, ctypes.c_void_p(cs.cuda_stream)) for b in range(nb)]
     used = [False] * nb
 
     def root_frame(f):
         b, k = f % nb, f & 1
-        if used[b]:
-            sts[k].wait_event(ev_a[b])                        # frame f - nb's unpack has read buffer b
-        abi.check(L.rt_render_dev_packed(*la[b], ctypes.c_void_p(sts[k].cuda_stream)), "rt_render_dev_packed")
-        ev_r[b].record(sts[k])
-        cs.wait_event(ev_r[b])
+        if root_renders:                                      # (an assembling rank 0: the unpack alone)
+            if used[b]:
+                sts[k].wait_event(ev_a[b])                    # frame f - nb's unpack has read buffer b
+            abi.check(L.rt_render_dev_packed(*la[b], ctypes.c_void_p(sts[k].cuda_stream)), "rt_render_dev_packed")
+            ev_r[b].record(sts[k])
+            cs.wait_event(ev_r[b])
         abi.check(L.rt_unpack_dev(*ub[b]), "rt_unpack_dev")
         ev_a[b].record(cs)
         used[b] = True
@@ -480,7 +490,7 @@ def c4_rank_projection(torch, L, abi, Tracer, cfg, dev, local, n, band_height, c
     torch.cuda.synchronize()
     root_ms = (time.perf_counter() - t0) * 1e3 / frames
     t.close()
-    keys = c4_projection_keys(n, c3_ms_per_frame, rank_ms, unpack_ms, sr * W, root_ms=root_ms)
+    keys = c4_projection_keys(n, c3_ms_per_frame, rank_ms, unpack_ms, sr * W, root_ms=root_ms, root_renders=root_renders)
     keys[f"n{n}_band_height"] = hb
     return keys
 
@@ -752,8 +762,9 @@ def main() -> int:
             arr = (ctypes.c_void_p * 1)(t._ctx.value)
             abi.check(L.rt_group_create(arr, 1, abi.RT_TRANSPORT_RCCL, ctypes.byref(g)), "rt_group_create")
         gw = copy_ranks or world                           # ranks of the group
-        band, slab = ctypes.c_int(), ctypes.c_int()
-        abi.check(L.rt_band_plan(H, gw, args.band_height, ctypes.byref(band), ctypes.byref(slab)), "rt_band_plan")
+        gp = abi.rt_group_plan()                           # the group's frame plan (rank 0's view of it)
+        abi.check(L.rt_group_plan_frame(W, H, gw, 0, args.band_height, abi.RT_OUT_RGBA8, 1, ctypes.byref(gp)),
+                  "rt_group_plan_frame")
         img8 = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
         argv = (g, ctypes.byref(cam), W, H, B, args.band_height, abi.RT_OUT_RGBA8,
                 None, ctypes.c_void_p(img8.data_ptr()) if img8 is not None else None, ctypes.c_void_p(stream.cuda_stream))
@@ -807,8 +818,8 @@ def main() -> int:
             e.close()
         info = {"ranks": gw, "rccl_world": 0 if copy_ranks else world,
                 "transport": "COPY (rehearsal: contexts share one GPU)" if copy_ranks else "RCCL",
-                "band_height": band.value,
-                "slab_rows": slab.value, "rays_per_frame": rays, "parity": parity,
+                "band_height": gp.band_height, "slab_rows": gp.slab_rows, "renderers": gp.renderers,
+                "root_renders": bool(gp.root_renders), "rays_per_frame": rays, "parity": parity,
                 "wire_format": names.get(st.wire_byte, st.wire_byte), "payload_bytes_to_rank0": st.payload_bytes,
                 "phases_ms_rank0": {k: round(v, 5) for k, v in phases.items()} if rank == 0 else None,
                 "phases_ms_max_over_ranks": phases_max,
@@ -837,19 +848,20 @@ def main() -> int:
         info, elapsed = group_leg(cfg, args.steps, args.warmup)
         rays_frame = info["rays_per_frame"]
         job_frames = 1
-        plan = BandPlan(H, world, args.band_height)
-        nl = plan.frame_local[rank]
-        # the kernel alone on this rank's rows, for the roofline
+        # the kernel alone on this rank's rows (the first renderer's when rank 0 only assembles), for the roofline
+        nr, ri = info["renderers"], rank if info["root_renders"] else max(rank - 1, 0)
+        plan = BandPlan(H, nr, info["band_height"])
+        nl = plan.frame_local[ri]
         tr = Tracer(local)
         tr.set_scene(scene)
-        bufs = tr.alloc(W, H, plan.rows(rank), rgba32f=True, rgba8=True)
+        bufs = tr.alloc(W, H, plan.rows(ri), rgba32f=True, rgba8=True)
         for _ in range(3):
-            tr.render_into(cam, W, H, B, bufs, rows=plan.rows(rank))
+            tr.render_into(cam, W, H, B, bufs, rows=plan.rows(ri))
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         torch.cuda.synchronize()
         e[0].record(stream)
         for _ in range(20):
-            tr.render_into(cam, W, H, B, bufs, rows=plan.rows(rank))
+            tr.render_into(cam, W, H, B, bufs, rows=plan.rows(ri))
         e[1].record(stream)
         torch.cuda.synchronize()
         avg_kern_ms = kern_serial_ms = e[0].elapsed_time(e[1]) / 20
@@ -1087,11 +1099,13 @@ def main() -> int:
                         proj.update(c4_rank_projection(torch, L, abi, Tracer, c3, dev, local, n, args.band_height,
                                                        base[0]))
                     proj["note"] = ("one-GPU projection of the c4 frame at n ranks (rt_render_multi at n > 1 needs n "
-                                    "GPUs): nN_rank_render_ms = each rank's band set rendered alone as the group "
-                                    "renders it (GRAY8 slab, two render streams taking frames in turn); nN_rank0_ms "
-                                    "= rank 0's pipeline as the group runs it (its bands, then per frame the unpack of "
-                                    "the gathered GRAY8 buffer into RGBA8 on a high-priority stream beside the next "
-                                    "render); nN_projected_frame_ms = the slowest of rank 0 and the peers (or the "
+                                    "GPUs): nN_rank_render_ms = each renderer's band set rendered alone as the group "
+                                    "renders it (GRAY8 slab, two render streams taking frames in turn; from 4 ranks the "
+                                    "renderers are ranks 1 .. n-1 and rank 0 only assembles, nN_root_renders); "
+                                    "nN_rank0_ms = rank 0's pipeline as the group runs it (its bands if it renders, "
+                                    "then per frame the unpack of the gathered GRAY8 buffer into RGBA8 on its comm "
+                                    "stream beside the next render, 3 frame buffers); nN_projected_frame_ms = the "
+                                    "slowest of rank 0 and the peers (or the "
                                     "nominal xGMI gather of one slab if longer); nN_speedup_bound = "
                                     "c3_1gpu_ms_per_frame / nN_projected_frame_ms")
                     info["projection"] = proj

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 #define RT_OK            0
 #define RT_EINVAL       -1   /* bad argument (null pointer, size, unsupported material, ...) */
@@ -333,13 +333,21 @@ typedef struct rt_group_plan {
     int32_t elem_bytes[2];       /* bytes per pixel of wire[k] */
     uint64_t slab_bytes[2];      /* this rank's slab per kind: slab_rows x width x elem_bytes */
     uint64_t send_bytes[2];      /* bytes this rank sends rank 0 per frame (0 on rank 0: its slab is unpacked in place) */
-    uint64_t gather_bytes[2];    /* rank 0: its gather buffer per kind (n_ranks slab-sized slots) */
+    uint64_t gather_bytes[2];    /* rank 0: its gather buffer per kind (one slab-sized slot per renderer) */
     uint64_t payload_bytes;      /* rank 0: bytes received from the other ranks per frame, all kinds */
+    int32_t renderers;           /* ranks that render bands: n_ranks, or n_ranks - 1 when rank 0 only assembles */
+    int32_t root_renders;        /* 1: rank 0 renders bands too; 0: bands go to ranks 1 .. n - 1 (rt_group_root_renders) */
 } rt_group_plan;
 /* The plan of `rank` for a width x height frame (band_height 0 = auto, `outputs` as rt_render_multi, achromatic =
- * rt_scene_achromatic of the group's scene). */
+ * rt_scene_achromatic of the group's scene).  The band plan is over the renderers (rt_rows {band_height, renderers,
+ * rank - (root_renders ? 0 : 1)}); rank 0 then receives every renderer's slab but its own. */
 int rt_group_plan_frame(int width, int height, int n_ranks, int rank, int band_height, int outputs, int achromatic,
                         rt_group_plan* out);
+/* Whether rank 0 of an n-rank group renders bands (1) or only receives and assembles the frame (0).  Rank 0 unpacks
+ * the whole image (an HBM-bound 33 MB of RGBA8 stores at 4K) and receives every peer's slab besides, so from 4 ranks
+ * on its bands go to the others (DESIGN.md §7 has the measurements); RT_GROUP_ROOT_RENDERS=0|1 overrides (every
+ * rank of a group must see the same setting). */
+int rt_group_root_renders(int n_ranks);
 /* Rank 0's receive from `peer` (1 .. n_ranks - 1) for image `kind`: byte offset into rank 0's gather buffer and
  * byte count (equal to that peer's send_bytes[kind]). */
 int rt_group_plan_recv(const rt_group_plan* plan, int width, int height, int peer, int kind, uint64_t* offset,

@@ -27,7 +27,7 @@ RT_MAX_DEPTH = 7
 RT_RAND_GLIBC, RT_RAND_MSVC = 0, 1
 RT_MESH_TETRAHEDRON = 1
 RT_MESH_CUBE = 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 RT_TRANSPORT_AUTO, RT_TRANSPORT_RCCL, RT_TRANSPORT_COPY = -1, 0, 1
 RT_OUT_RGBA32F, RT_OUT_RGBA8 = 1, 2
 RT_PIXEL_RGBA32F, RT_PIXEL_GRAY32F, RT_PIXEL_RGBA8, RT_PIXEL_RGB8, RT_PIXEL_GRAY8 = 0, 1, 2, 3, 4
@@ -108,7 +108,7 @@ class rt_group_plan(Structure):
     _fields_ = [("n_ranks", c_int32), ("rank", c_int32), ("band_height", c_int32), ("slab_rows", c_int32),
                 ("rank_rows", c_int32), ("wire", c_int32 * 2), ("elem_bytes", c_int32 * 2),
                 ("slab_bytes", c_uint64 * 2), ("send_bytes", c_uint64 * 2), ("gather_bytes", c_uint64 * 2),
-                ("payload_bytes", c_uint64)]
+                ("payload_bytes", c_uint64), ("renderers", c_int32), ("root_renders", c_int32)]
 
 
 class RtError(RuntimeError):
@@ -169,6 +169,7 @@ SIGNATURES = {
     "rt_unpack_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "rt_group_plan_frame": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, _P(rt_group_plan)]),
     "rt_group_plan_recv": (c_int, [_P(rt_group_plan), c_int, c_int, c_int, c_int, _P(c_uint64), _P(c_uint64)]),
+    "rt_group_root_renders": (c_int, [c_int]),
     "rt_scene_fingerprint": (c_int, [_P(rt_scene), _P(c_uint64)]),
     # include/rt_diag.h
     "rt_group_agree_due": (c_int, [c_uint64, c_int, c_uint64]),

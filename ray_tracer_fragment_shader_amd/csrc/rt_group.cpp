@@ -488,6 +488,9 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
     const std::vector<rt_group_plan>& plan = g->plan;
     const rt_group_plan& root_plan = g->root_plan;
     const int hb = root_plan.band_height, slab_rows = root_plan.slab_rows;
+    // rank 0 renders bands too (root_renders), or bands go to ranks 1 .. n - 1 (renderers) and it only assembles
+    const bool root_renders = root_plan.root_renders != 0;
+    const int renderers = root_plan.renderers;
     // (the render call takes a format for an image it does not write too)
     const int wire[kKinds] = {achro ? RT_PIXEL_GRAY32F : RT_PIXEL_RGBA32F, achro ? RT_PIXEL_GRAY8 : RT_PIXEL_RGB8};
     for (int k = 0; k < kKinds; ++k) g->last_wire[k] = root_plan.wire[k];
@@ -574,10 +577,12 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         if (r.rank == 0 && g->assembled_rec[b])                               // the root's slab[b] is read by
             G_HIP(hipStreamWaitEvent(rs, g->assembled[b], 0));                // frame - n_bufs's unshuffle
         if (pe[q]) G_HIP(hipEventRecord(pe[q]->r0, rs));
-        rt_rows rows = {hb, g->n_ranks, r.rank, 1};
-        rc = rt_render_dev_packed(r.ctx, cam, W, H, depth, &rows, wire[0], kind_on[0] ? r.slab[b][0] : nullptr,
-                                  wire[1], kind_on[1] ? r.slab[b][1] : nullptr, rs);
-        if (rc) return rc;
+        if (r.rank != 0 || root_renders) {                   // (an assembling rank 0 renders nothing)
+            rt_rows rows = {hb, renderers, root_renders ? r.rank : r.rank - 1, 1};
+            rc = rt_render_dev_packed(r.ctx, cam, W, H, depth, &rows, wire[0], kind_on[0] ? r.slab[b][0] : nullptr,
+                                      wire[1], kind_on[1] ? r.slab[b][1] : nullptr, rs);
+            if (rc) return rc;
+        }
         G_HIP(hipSetDevice(r.device));
         if (pe[q]) G_HIP(hipEventRecord(pe[q]->r1, rs));
         G_HIP(hipEventRecord(r.rendered[b], rs));
@@ -675,11 +680,11 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         G_HIP(hipSetDevice(root.device));
         G_HIP(hipEventRecord(g->received[b], st));                   // caller's earlier work on the image
         G_HIP(hipStreamWaitEvent(root.cs, g->received[b], 0));
-        G_HIP(hipStreamWaitEvent(root.cs, root.rendered[b], 0));     // the root's own slab
+        if (root_renders) G_HIP(hipStreamWaitEvent(root.cs, root.rendered[b], 0));     // the root's own slab
         for (int k = 0; k < kKinds; ++k) {
             if (!kind_on[k]) continue;
-            rc = rt_unpack_dev_ex(g->gathered[b][k], root.slab[b][k], outs[k], W, H, wire[k], kImageFormat[k], hb,
-                                  g->n_ranks, slab_rows, root.cs);
+            rc = rt_unpack_dev_ex(g->gathered[b][k], root_renders ? root.slab[b][k] : nullptr, outs[k], W, H, wire[k],
+                                  kImageFormat[k], hb, renderers, slab_rows, root.cs);
             if (rc) return rc;
         }
         G_HIP(hipSetDevice(root.device));

@@ -7,6 +7,7 @@
 // multi-GPU split is this build's.  Pixels are independent (rayTraceRay :1184-1249 reads only the
 // scene), so a frame splits into round-robin row bands (rt_band_plan) gathered to rank 0.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/rt_api.h"
@@ -25,6 +26,11 @@ int local_rows(int height, int band, int n_ranks, int rank) {
 
 }  // namespace
 
+extern "C" int rt_group_root_renders(int n_ranks) {
+    if (const char* e = getenv("RT_GROUP_ROOT_RENDERS")) return atoi(e) != 0 ? 1 : 0;
+    return n_ranks < 4 ? 1 : 0;
+}
+
 extern "C" int rt_group_plan_frame(int width, int height, int n_ranks, int rank, int band_height, int outputs,
                                    int achromatic, rt_group_plan* out) {
     if (!out || width <= 0 || height <= 0 || n_ranks <= 0 || rank < 0 || rank >= n_ranks)
@@ -33,11 +39,15 @@ extern "C" int rt_group_plan_frame(int width, int height, int n_ranks, int rank,
         return rt_fail(RT_EINVAL, "rt_group_plan_frame: outputs must be a non-empty set of RT_OUT_RGBA32F | RT_OUT_RGBA8");
     rt_group_plan p;
     std::memset(&p, 0, sizeof(p));
-    int rc = rt_band_plan(height, n_ranks, band_height, &p.band_height, &p.slab_rows);
+    // the bands go to the renderers: every rank, or ranks 1 .. n - 1 when rank 0 only assembles
+    p.root_renders = n_ranks == 1 ? 1 : rt_group_root_renders(n_ranks);
+    p.renderers = p.root_renders ? n_ranks : n_ranks - 1;
+    const int rr = p.root_renders ? rank : rank - 1;           // this rank's renderer index, -1: none
+    int rc = rt_band_plan(height, p.renderers, band_height, &p.band_height, &p.slab_rows);
     if (rc) return rc;
     p.n_ranks = n_ranks;
     p.rank = rank;
-    p.rank_rows = local_rows(height, p.band_height, n_ranks, rank);
+    p.rank_rows = rr >= 0 ? local_rows(height, p.band_height, p.renderers, rr) : 0;
     if (p.rank_rows < 0) return rt_fail(RT_EINVAL, "rt_group_plan_frame: row plan");
     // Wire formats: the narrowest exact one (GRAY for achromatic scenes, whose pixels have R = G = B bit for bit)
     const bool on[kKinds] = {(outputs & RT_OUT_RGBA32F) != 0, (outputs & RT_OUT_RGBA8) != 0};
@@ -48,13 +58,14 @@ extern "C" int rt_group_plan_frame(int width, int height, int n_ranks, int rank,
         int pb = 0;
         if ((rc = rt_pixel_bytes(wire[k], &pb))) return rc;
         p.elem_bytes[k] = pb;
-        p.slab_bytes[k] = (uint64_t)p.slab_rows * width * pb;
+        const uint64_t slot = (uint64_t)p.slab_rows * width * pb;
+        p.slab_bytes[k] = rr >= 0 ? slot : 0;                   // (an assembling rank 0 has no slab)
         // rank 0 unpacks its own slab in place instead of sending it to itself
         p.send_bytes[k] = rank == 0 || n_ranks == 1 ? 0 : (uint64_t)p.rank_rows * width * pb;
         if (rank == 0 && n_ranks > 1) {
-            p.gather_bytes[k] = (uint64_t)n_ranks * p.slab_bytes[k];
-            for (int q = 1; q < n_ranks; ++q)
-                p.payload_bytes += (uint64_t)local_rows(height, p.band_height, n_ranks, q) * width * pb;
+            p.gather_bytes[k] = (uint64_t)p.renderers * slot;
+            for (int r = p.root_renders ? 1 : 0; r < p.renderers; ++r)
+                p.payload_bytes += (uint64_t)local_rows(height, p.band_height, p.renderers, r) * width * pb;
         }
     }
     *out = p;
@@ -67,11 +78,12 @@ extern "C" int rt_group_plan_recv(const rt_group_plan* p, int width, int height,
         width <= 0 || height <= 0)
         return rt_fail(RT_EINVAL, "rt_group_plan_recv: bad arguments (rank 0's plan, peers 1 .. n_ranks - 1)");
     if (p->wire[kind] < 0) return rt_fail(RT_EINVAL, "rt_group_plan_recv: that image is not requested");
-    const int nl = local_rows(height, p->band_height, p->n_ranks, peer);
+    const int rr = p->root_renders ? peer : peer - 1;         // the peer's renderer index
+    const int nl = local_rows(height, p->band_height, p->renderers, rr);
     if (nl < 0) return rt_fail(RT_EINVAL, "rt_group_plan_recv: row plan");
-    // peer q's rows land in its own slab-sized slot of rank 0's gather buffer (slot 0 stays unused: rank 0's rows
-    // are read from its slab by the unpack), which is the layout rt_unpack_dev reads
-    *offset = (uint64_t)peer * p->slab_bytes[kind];
+    // the peer's rows land in its renderer's slab-sized slot of rank 0's gather buffer (when rank 0 renders, slot 0
+    // stays unused: its rows are read from its own slab by the unpack), which is the layout rt_unpack_dev reads
+    *offset = (uint64_t)rr * p->slab_rows * width * p->elem_bytes[kind];
     *bytes = (uint64_t)nl * width * p->elem_bytes[kind];
     return RT_OK;
 }

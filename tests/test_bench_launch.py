@@ -143,6 +143,12 @@ def test_c4_projection_keys():
     m = bench.c4_projection_keys(8, 0.112, [0.015, 0.0165, 0.016], 0.003, 1_044_480, root_ms=0.016)
     assert m["n8_projected_frame_ms"] == 0.0165 and m["n8_limiting_stage"] == "a peer's band render"
     assert m["n8_speedup_bound"] == round(0.112 / 0.0165, 3)
+    # rank 0 only assembles: the seven renderers are all peers, rank 0 is its unpack pipeline
+    a = bench.c4_projection_keys(8, 0.112, [0.016] * 6 + [0.017], 0.007, 1_200_000, root_ms=0.0075, root_renders=False)
+    assert a["n8_root_renders"] is False and a["n8_projected_frame_ms"] == 0.017
+    assert a["n8_limiting_stage"] == "a peer's band render" and a["n8_speedup_bound"] == round(0.112 / 0.017, 3)
+    b = bench.c4_projection_keys(8, 0.112, [0.016] * 7, 0.02, 1_200_000, root_renders=False)
+    assert b["n8_rank0_ms"] == 0.02 and b["n8_limiting_stage"] == "rank 0 (unpack)"
     slow = bench.c4_projection_keys(8, 0.112, [0.001], 0.0005, 10_000_000)      # gather-bound
     assert slow["n8_limiting_stage"] == "gather (nominal xGMI)"
     assert slow["n8_projected_frame_ms"] == slow["n8_gather_ms_nominal"]

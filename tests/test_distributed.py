@@ -187,9 +187,13 @@ def _protocol_worker(rank, world, port, W, H, scene_names, outputs, out_path):
         sends = torch.tensor([int(plan.send_bytes[0]), int(plan.send_bytes[1])], dtype=torch.int64)
         all_sends = [torch.empty_like(sends) for _ in range(world)]
         dist.all_gather(all_sends, sends)
-        rows = abi.rt_rows(plan.band_height, world, rank, 1)
-        rgb, _ = po.render(s_abi, cfg.camera(W, H) if cfg else scenes.CONFIGS["c2"].camera(W, H), W, H,
-                           cfg.depth if cfg else 1, rows=rows, nthreads=1)
+        rr = rank if plan.root_renders else rank - 1          # this rank's renderer index (-1: rank 0 only assembles)
+        if rr >= 0:
+            rows = abi.rt_rows(plan.band_height, plan.renderers, rr, 1)
+            rgb, _ = po.render(s_abi, cfg.camera(W, H) if cfg else scenes.CONFIGS["c2"].camera(W, H), W, H,
+                               cfg.depth if cfg else 1, rows=rows, nthreads=1)
+        else:
+            rgb = np.zeros((0, W, 3))
         assert rgb.shape[0] == plan.rank_rows
         kinds = [k for k in range(2) if plan.wire[k] >= 0]
         if rank == 0:
@@ -203,7 +207,9 @@ def _protocol_worker(rank, world, port, W, H, scene_names, outputs, out_path):
                                                    ctypes.byref(nb)), "rt_group_plan_recv")
                     # both sides of every send / recv carry the same byte count
                     assert nb.value == int(all_sends[q][k]), (q, k, nb.value, int(all_sends[q][k]))
-                    assert off.value + nb.value <= plan.gather_bytes[k] and off.value >= plan.slab_bytes[k] * q
+                    slot_bytes = plan.slab_rows * W * plan.elem_bytes[k]
+                    assert off.value + nb.value <= plan.gather_bytes[k]
+                    assert off.value == slot_bytes * (q if plan.root_renders else q - 1)
                     buf = torch.empty(nb.value, dtype=torch.uint8)
                     dist.recv(buf, src=q)
                     gathered[k][off.value: off.value + nb.value] = buf.numpy()
@@ -213,12 +219,13 @@ def _protocol_worker(rank, world, port, W, H, scene_names, outputs, out_path):
             img = {}
             for k in kinds:
                 eb = plan.elem_bytes[k]
-                own = np.ascontiguousarray(_pack_wire(rgb, plan.wire[k])).view(np.uint8).reshape(-1)
-                slot = gathered[k].reshape(world, int(plan.slab_bytes[k]))
-                slot[0, : own.size] = own
+                slot = gathered[k].reshape(plan.renderers, plan.slab_rows * W * eb)
+                if plan.root_renders:
+                    own = np.ascontiguousarray(_pack_wire(rgb, plan.wire[k])).view(np.uint8).reshape(-1)
+                    slot[0, : own.size] = own
                 out = np.zeros((H, W * eb), np.uint8)
-                for q in range(world):
-                    rq = abi.rt_rows(plan.band_height, world, q, 1)
+                for q in range(plan.renderers):
+                    rq = abi.rt_rows(plan.band_height, plan.renderers, q, 1)
                     nl = ctypes.c_int()
                     abi.check(L.rt_local_rows(H, ctypes.byref(rq), ctypes.byref(nl)), "rt_local_rows")
                     for lr in range(nl.value):
@@ -249,6 +256,7 @@ def _chromatic_scene():
 @pytest.mark.parametrize("world,names,outputs", [
     (2, ("c2", "c2"), 3),            # achromatic: GRAY32F + GRAY8
     (3, ("chroma",) * 3, 2),         # chromatic, RGBA8 only: RGB8
+    (4, ("c2",) * 4, 2),             # rank 0 only assembles: the bands go to ranks 1 .. 3
 ])
 def test_group_protocol_plan_and_gather(tmp_path, world, names, outputs):
     from oracle import pyoracle as po
@@ -282,29 +290,53 @@ def test_group_protocol_scene_mismatch_fails_on_every_rank(tmp_path):
         assert int(np.load(f"{prefix}_{r}.npy")[0]) == abi.RT_EINVAL
 
 
-def test_group_plan_matches_band_plan():
-    """rt_group_plan_frame against the band plan and pixel sizes it is built from, for the bench sizes."""
+@pytest.mark.parametrize("root_env", [None, "0", "1"])
+def test_group_plan_matches_band_plan(monkeypatch, root_env):
+    """rt_group_plan_frame against the band plan and pixel sizes it is built from, for the bench sizes: rank 0 renders
+    bands below 4 ranks and only assembles from 4 on (rt_group_root_renders; RT_GROUP_ROOT_RENDERS forces either), the
+    bands then going to ranks 1 .. n - 1."""
     from ray_tracer_fragment_shader_amd import abi
+    if root_env is None:
+        monkeypatch.delenv("RT_GROUP_ROOT_RENDERS", raising=False)
+    else:
+        monkeypatch.setenv("RT_GROUP_ROOT_RENDERS", root_env)
     L = abi.lib()
+    for n in (1, 2, 3, 4, 8):
+        want = 1 if n == 1 else (int(root_env) if root_env is not None else int(n < 4))
+        assert (L.rt_group_root_renders(n) if n > 1 else 1) == want
     for W, H in ((1920, 1080), (3840, 2160), (7680, 4320), (97, 61)):
-        for n in (1, 2, 3, 8):
+        for n in (1, 2, 3, 4, 8):
             for achro in (0, 1):
                 plans = []
                 for r in range(n):
                     p = abi.rt_group_plan()
                     abi.check(L.rt_group_plan_frame(W, H, n, r, 0, 3, achro, ctypes.byref(p)), "plan")
                     plans.append(p)
+                root = plans[0].root_renders
+                assert root == (1 if n == 1 else L.rt_group_root_renders(n))
+                assert all(p.renderers == (n if root else n - 1) and p.root_renders == root for p in plans)
                 hb, slab = ctypes.c_int(), ctypes.c_int()
-                abi.check(L.rt_band_plan(H, n, 0, ctypes.byref(hb), ctypes.byref(slab)), "rt_band_plan")
+                abi.check(L.rt_band_plan(H, plans[0].renderers, 0, ctypes.byref(hb), ctypes.byref(slab)), "rt_band_plan")
                 assert all(p.band_height == hb.value and p.slab_rows == slab.value for p in plans)
                 assert sum(p.rank_rows for p in plans) == H
+                if not root:
+                    assert plans[0].rank_rows == 0
                 eb = (4, 1) if achro else (16, 3)
                 for k in range(2):
-                    assert all(p.elem_bytes[k] == eb[k] and p.slab_bytes[k] == slab.value * W * eb[k] for p in plans)
+                    renders = [p for p in plans if p.rank != 0 or root]
+                    assert all(p.elem_bytes[k] == eb[k] and p.slab_bytes[k] == slab.value * W * eb[k] for p in renders)
+                    assert root or plans[0].slab_bytes[k] == 0
                     assert sum(p.send_bytes[k] for p in plans) == (H - plans[0].rank_rows) * W * eb[k] * (n > 1)
                 assert plans[0].payload_bytes == sum(p.send_bytes[0] + p.send_bytes[1] for p in plans[1:])
                 if n > 1:
-                    assert plans[0].gather_bytes[1] == n * plans[0].slab_bytes[1]
+                    assert plans[0].gather_bytes[1] == plans[0].renderers * slab.value * W * eb[1]
+                    # the receive table tiles the gather buffer: one renderer slot per peer, in renderer order
+                    for q in range(1, n):
+                        off, nb = ctypes.c_uint64(), ctypes.c_uint64()
+                        abi.check(L.rt_group_plan_recv(ctypes.byref(plans[0]), W, H, q, 1, ctypes.byref(off),
+                                                       ctypes.byref(nb)), "recv")
+                        assert off.value == (q if root else q - 1) * slab.value * W * eb[1]
+                        assert nb.value == plans[q].send_bytes[1]
     # misuse: a receive table asked of a rank other than 0, or of a peer out of range
     p = abi.rt_group_plan()
     abi.check(L.rt_group_plan_frame(64, 64, 2, 1, 0, 3, 1, ctypes.byref(p)), "plan")
