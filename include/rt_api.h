@@ -389,7 +389,7 @@ typedef struct rt_group_stats {
     int32_t wire_byte;           /* RT_PIXEL_* sent for RT_OUT_RGBA8, -1: not requested (last frame) */
     int32_t ranks_timed;         /* this process's ranks the means are over */
     uint64_t payload_bytes;      /* bytes rank 0 receives from the other ranks per frame (last frame) */
-    double render_ms;            /* mean rt_render_dev launch on a rank's render stream */
+    double render_ms;            /* mean rt_render_dev launch on a rendering rank's render stream */
     double gather_ms;            /* mean send (rank > 0) / receive of every peer's slab (rank 0), from the
                                     point the rank's own render is done (it includes waiting for peers) */
     double assemble_ms;          /* rank 0: unshuffle + expand into the images (0 elsewhere) */

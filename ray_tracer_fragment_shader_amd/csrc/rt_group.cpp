@@ -62,6 +62,7 @@ constexpr int kBufs = 3;
 struct PhaseEvents {
     hipEvent_t r0 = nullptr, r1 = nullptr, g0 = nullptr, g1 = nullptr, a1 = nullptr;
     bool rec = false, gather_rec = false;
+    bool rendered = true;                      // false: an assembling rank 0 (r0 .. r1 is empty, not a render)
 };
 
 struct Rank {
@@ -392,7 +393,7 @@ extern "C" int rt_group_get_stats(rt_group* g, rt_group_stats* st) {
             if (q == 0 && g->owns_root && e.a1) G_HIP(hipEventSynchronize(e.a1));
             float ms = 0.f;
             G_HIP(hipEventElapsedTime(&ms, e.r0, e.r1));
-            sr += ms, ++nr;
+            if (e.rendered) sr += ms, ++nr;
             if (e.gather_rec) {
                 G_HIP(hipEventElapsedTime(&ms, e.g0, e.g1));
                 sg += ms, ++ng;
@@ -576,7 +577,10 @@ extern "C" int rt_render_multi(rt_group* g, const rt_camera* cam, int W, int H, 
         if (r.sent_rec[b]) G_HIP(hipStreamWaitEvent(rs, r.sent[b], 0));       // slab[b] has left (frame - n_bufs)
         if (r.rank == 0 && g->assembled_rec[b])                               // the root's slab[b] is read by
             G_HIP(hipStreamWaitEvent(rs, g->assembled[b], 0));                // frame - n_bufs's unshuffle
-        if (pe[q]) G_HIP(hipEventRecord(pe[q]->r0, rs));
+        if (pe[q]) {
+            G_HIP(hipEventRecord(pe[q]->r0, rs));
+            pe[q]->rendered = r.rank != 0 || root_renders;
+        }
         if (r.rank != 0 || root_renders) {                   // (an assembling rank 0 renders nothing)
             rt_rows rows = {hb, renderers, root_renders ? r.rank : r.rank - 1, 1};
             rc = rt_render_dev_packed(r.ctx, cam, W, H, depth, &rows, wire[0], kind_on[0] ? r.slab[b][0] : nullptr,

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """draw()'s host-frame path at c2 (GRAY8, pinned): A/B of where the device-to-host copy runs.
 
-Settings (env read at rt_ctx_create; SETTINGS=mode:blocks[:split[:chunks]]): RT_COPY_MODE 1 = copy kernel on the render stream (serial), 0 = copy kernel
+Settings (env read at rt_ctx_create; SETTINGS=mode:blocks[:split[:chunks[:writer]]]): RT_COPY_MODE 1 = copy kernel on the render stream (serial), 0 = copy kernel
 on the context's copy stream (overlaps the next render), 2 = the render kernel stores straight into the pinned
 host buffer (no copy), 3 = an SDMA engine copies it (HSA, no CUs); RT_COPY_BLOCKS = copy-kernel workgroups (0 = auto,
 up to 1024).  Every setting's frames are
@@ -21,8 +21,9 @@ from ray_tracer_fragment_shader_amd import abi, scenes  # noqa: E402
 from ray_tracer_fragment_shader_amd.tracer import Tracer  # noqa: E402
 
 # mode:blocks[:split[:chunks]] — RT_SDMA_SPLIT (engines an SDMA frame copy is split over); RT_SDMA_CHUNKS (row chunks
-# of a synchronous SDMA frame) was an r05 experiment, no longer read
-SETTINGS = [tuple((x + ":2:2:2").split(":")[:4]) for x in
+# of a synchronous SDMA frame) was an r05 experiment, no longer read; writer = RT_SDMA_WRITER (how the render stream
+# starts the SDMA copy: 1 stream write-value, 2 signal kernel, 0 the library's choice)
+SETTINGS = [tuple((x + ":2:2:2:0").split(":")[:5]) for x in
             os.environ.get("SETTINGS", "1:0,0:0,0:64,0:16,1:64,2:0").split(",")]
 # (RT_COPY_KERNEL=0 in the environment: hipMemcpyAsync — the runtime's blit kernel — instead of the copy kernel)
 L = abi.lib()
@@ -35,10 +36,11 @@ _, want = ref.render_packed(cam, W, H, B, byte_format=abi.RT_PIXEL_GRAY8)
 torch.cuda.synchronize()
 want = want.cpu().numpy().reshape(-1)
 ctxs = {}
-for mode, blocks, split, chunks in SETTINGS:
+for mode, blocks, split, chunks, writer in SETTINGS:
     os.environ["RT_COPY_MODE"], os.environ["RT_COPY_BLOCKS"] = mode, blocks
     os.environ["RT_SDMA_SPLIT"], os.environ["RT_SDMA_CHUNKS"] = split, chunks
-    ctxs[(mode, blocks, split, chunks)] = Tracer(0)
+    os.environ["RT_SDMA_WRITER"] = writer
+    ctxs[(mode, blocks, split, chunks, writer)] = Tracer(0)
 pins = []
 for _ in range(3):
     p = ctypes.c_void_p()
@@ -72,8 +74,8 @@ for rnd in range(int(os.environ.get("ROUNDS", "5"))):
             for j in range(3):
                 got = (ctypes.c_uint8 * (W * H)).from_address(pins[j].value)
                 assert np.array_equal(np.frombuffer(got, np.uint8), want), f"{key}: pipelined frame differs"
-out = {f"mode{m}_blocks{b}" + (f"_split{sp}_chunks{ch}" if m == "3" else ""):
-       {n: round(statistics.median(v), 1) for n, v in d.items()} for (m, b, sp, ch), d in res.items()}
+out = {f"mode{m}_blocks{b}" + (f"_split{sp}_writer{w}" if m == "3" else ""):
+       {n: round(statistics.median(v), 1) for n, v in d.items()} for (m, b, sp, ch, w), d in res.items()}
 print(json.dumps({"us_per_frame_median": out, "frames": k}, indent=1))
 for p in pins:
     L.rt_host_free(p)

@@ -20,6 +20,7 @@
 #   queues    tools/c4_gap_probe.py part 5, plain and under --kernel-trace (hardware queue of each stream kind)
 #   c4probe   tools/c4_gap_probe.py (PARTS, NS, HBS)
 #   count     tools/count.sh (PMC instruction counts per scene variant, VARIANTS)
+#   profsdma  tools/prof_sdma.sh (kernel + memory-copy trace of the SDMA host-frame path)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -115,6 +116,9 @@ if want c4probe; then
 fi
 if want count; then
   timeout -k 10 400 bash tools/count.sh || { echo "count failed"; exit 35; }
+fi
+if want profsdma; then
+  timeout -k 10 300 bash tools/prof_sdma.sh || { echo "prof_sdma failed"; exit 36; }
 fi
 if want bench; then
   timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" \
