@@ -421,6 +421,60 @@ __device__ __forceinline__ bool bound_pass(const DevScene* S, d3 p0, d3 u) {
 // CheckerBoard -> Quad -> Triangle T1 then T2, first hit wins (:1097, :817, :611-707).
 // d = end - start (unnormalised, :647).  Returns the hit point in *p.  PRIMARY: p0 is the camera eye and
 // the numerator n . (v0 - eye) was computed for it by rt_prepare_kernel with the same operations.
+// RT_BOARD_FLAT=1: the same decisions with one divergent region per outcome instead of one per early return (the
+// sign tests and the numerator evaluated for every lane, the position decision and the exact triangles folded into
+// one hit flag): fewer exec-mask save / restore pairs in the scalar stream (DESIGN.md §9, c2 SALU attribution).
+#ifndef RT_BOARD_FLAT
+#define RT_BOARD_FLAT 1
+#endif
+#if RT_BOARD_FLAT
+template <bool PRIMARY = false>
+__device__ __forceinline__ bool board_hit(const DevScene* S, d3 p0, d3 d, d3* p) {
+    const DevTri& T = S->tri[0];
+    d3 n = ld3(T.n);
+    double nd = dot(n, d);                                  // :648
+    d3 v0 = ld3(T.v0);
+    double num = PRIMARY ? S->board_num : dot(n, sub(v0, p0));   // :657 numerator
+    // :651 and the sign half of :659 (m = num / nd <= 0 misses), as in the branchy version below
+    const bool live = !(fabs(nd) < S->eps) & !((num == 0.0) | ((num < 0.0) != (nd < 0.0)));
+    bool hit = false;
+    if (live) {
+        double m = num / nd;                                // :657
+        if (!(m < S->eps)) {                                // :659
+            d3 q = add(p0, scl(m, d));                      // :665
+            d3 w = sub(q, v0);                              // :667
+            bool decided = false;
+#if RT_BOARD_POS
+            if (S->board_fast) {                            // (the position decision of the branchy version)
+                const double wx = w.x, wz = w.z, lo = S->board_lo, hi = S->board_hi, diag = fabs(wx - wz);
+                const double far = S->board_far, out = S->board_out, ax = fabs(wx), az = fabs(wz);
+                const bool in = (wx >= lo) & (wz >= lo) & (wx <= hi) & (wz <= hi) & (diag >= lo);
+                const bool outside = (ax <= far) & (az <= far) & ((wx <= -lo) | (wz <= -lo) | (wx >= out) | (wz >= out));
+                hit = in;
+                decided = in | outside;
+            }
+#endif
+            if (!decided) {
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const DevTri& Tt = S->tri[t];
+                    double wu = dot(w, ld3(Tt.u));          // :670
+                    double wv = dot(w, ld3(Tt.v));          // :671
+                    double A = Tt.uv * wv - Tt.vv * wu;
+                    double B = Tt.uv * wu - Tt.uu * wv;
+                    if (!hit & !(A > Tt.thr || B > Tt.thr)) {
+                        double s = div_const(A, Tt.den, Tt.rden, Tt.fast);   // :673
+                        double tt = div_const(B, Tt.den, Tt.rden, Tt.fast);  // :674
+                        hit = (s >= 0) & (tt >= 0) & (s + tt <= 1);          // :676
+                    }
+                }
+            }
+            if (hit) *p = q;
+        }
+    }
+    return hit;
+}
+#else
 template <bool PRIMARY = false>
 __device__ __forceinline__ bool board_hit(const DevScene* S, d3 p0, d3 d, d3* p) {
     const DevTri& T = S->tri[0];
@@ -478,6 +532,8 @@ __device__ __forceinline__ bool board_hit(const DevScene* S, d3 p0, d3 d, d3* p)
     }
     return false;
 }
+
+#endif
 
 // Tests that a ray starting at the hit point q of the previous level certainly misses (exact skips):
 //  * the board, when q is a board hit of a ray from p0.  The board normal is exactly (0, -1, 0) (host-
