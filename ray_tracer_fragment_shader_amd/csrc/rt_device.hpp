@@ -1150,6 +1150,73 @@ __device__ __forceinline__ uint64_t shadow_bundle_mask(const SceneView& V, bool 
 // far inside the 2^-16 folded into c_k; the FP64 hit test's own rounding moves the line by ~1e-13
 // relative, likewise covered.  A NaN direction is not rejected (it compares false), as the FP64 test
 // reports NaN rays as hits.
+// RT_OCCL_FLAT=1: the same any-hit test with a per-lane flag instead of returns from inside the sphere loops (a lane
+// that found a blocker leaves the loops; the board is tested by the lanes still unblocked).
+#ifndef RT_OCCL_FLAT
+#define RT_OCCL_FLAT 1
+#endif
+#if RT_OCCL_FLAT
+template <bool FULL, bool CULL = false>
+__device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull,
+                                         int skip = -1) {
+    const DevScene* S = V.S;
+    if (!(RT_HITS_INSIDE && (RT_HITS_VIEW ? V.hits_ok : S->hits_ok)) && !bound_pass(S, r.p0, r.u)) return false;   // shadow rays start at hits
+    const double eps = S->eps;
+    const DevSphereLightF* lf = V.lightf + li * V.ns;
+    bool blocked = false;
+    int k0 = 0;
+    if (CULL && V.np >= kConeMin) {                               // mask: shadow_bundle_mask
+        for (uint64_t m = mask & sphere_bits(V.np); m; m &= m - 1) {
+            const int k = __builtin_ctzll(m);
+            const DevSphereLightF& f = lf[k];
+            float t = r.ux * f.vx;
+            t = fmaf(r.uy, f.vy, t);
+            t = fmaf(r.uz, f.vz, t);
+            RT_COUNT(S, kCntFilterShadow, 1);
+            RT_COUNT_LANES(S, kCntLanesFilterShadow);
+            if (blocked | (fabsf(t) < f.c) | (k == skip - 1)) continue;
+            RT_COUNT(S, kCntExactShadow, 1);
+            RT_COUNT_LANES(S, kCntLanesExactShadow);
+            d3 q;
+            blocked = sphere_hit(V.sph[k], r.p0, r.u, eps, &q);
+        }
+        k0 = 64;
+    }
+    for (; k0 < V.np; k0 += kChunk) {
+        if (k0 < 64 && ((mask >> k0) & ((1ull << kChunk) - 1)) == 0) continue;   // (cached masks, as closest_hit)
+        uint32_t pass = 0;
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            const DevSphereLightF& f = lf[k0 + j];
+            float t = r.ux * f.vx;
+            t = fmaf(r.uy, f.vy, t);
+            t = fmaf(r.uz, f.vz, t);
+            pass |= (fabsf(t) < f.c ? 0u : 1u) << j;
+        }
+        pass = blocked ? 0u : drop_self(pass, skip - 1, k0);
+        while (pass) {
+            const int k = k0 + __builtin_ctz(pass);
+            d3 q;
+            blocked = sphere_hit(V.sph[k], r.p0, r.u, eps, &q);
+            pass = blocked ? 0u : pass & (pass - 1);
+        }
+    }
+    if (S->has_board && skip != 0 && !blocked) {
+        d3 q;
+        RT_COUNT(S, kCntBoardShadow, 1);
+        blocked = board_hit(S, r.p0, r.d, &q);
+    }
+    for (int m = 0; FULL && m < V.nm; ++m) {
+        const DevMesh& M = V.mesh[m];
+        if (blocked || !mesh_bound(M, r.p0, r.u, eps)) continue;
+        for (int t = M.tri0; t < M.tri0 + M.nfaces * M.per_face && !blocked; ++t) {
+            d3 q;
+            blocked = tri_hit(V.tri[t], r.p0, r.d, eps, &q);
+        }
+    }
+    return blocked;
+}
+#else
 template <bool FULL, bool CULL = false>
 __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull,
                                          int skip = -1) {
@@ -1216,6 +1283,8 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
     }
     return false;
 }
+
+#endif
 
 // Material of a hit (checker parity for the board, :1101-1111).
 // (int)(x / square) for the checker, both quotients sharing one reciprocal r = rcp_core(square) (the
