@@ -1151,14 +1151,15 @@ __device__ __forceinline__ uint64_t shadow_bundle_mask(const SceneView& V, bool 
 // relative, likewise covered.  A NaN direction is not rejected (it compares false), as the FP64 test
 // reports NaN rays as hits.
 // RT_OCCL_FLAT=1: the same any-hit test with a per-lane flag instead of returns from inside the sphere loops (a lane
-// that found a blocker leaves the loops; the board is tested by the lanes still unblocked).
+// that found a blocker leaves the loops; the board is tested by the lanes still unblocked).  occluded<.., FLAT> picks
+// the form per instance (shade: the three-channel culling kernels keep the returns — the flag form spills 32 VGPRs
+// to scratch in their depth-3 instance).
 #ifndef RT_OCCL_FLAT
 #define RT_OCCL_FLAT 1
 #endif
-#if RT_OCCL_FLAT
 template <bool FULL, bool CULL = false>
-__device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull,
-                                         int skip = -1) {
+__device__ __forceinline__ bool occluded_flag(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull,
+                                              int skip = -1) {
     const DevScene* S = V.S;
     if (!(RT_HITS_INSIDE && (RT_HITS_VIEW ? V.hits_ok : S->hits_ok)) && !bound_pass(S, r.p0, r.u)) return false;   // shadow rays start at hits
     const double eps = S->eps;
@@ -1216,10 +1217,10 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
     }
     return blocked;
 }
-#else
+
 template <bool FULL, bool CULL = false>
-__device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull,
-                                         int skip = -1) {
+__device__ __forceinline__ bool occluded_ret(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull,
+                                             int skip = -1) {
     const DevScene* S = V.S;
     if (!(RT_HITS_INSIDE && (RT_HITS_VIEW ? V.hits_ok : S->hits_ok)) && !bound_pass(S, r.p0, r.u)) return false;   // shadow rays start at hits
     const double eps = S->eps;
@@ -1284,7 +1285,12 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
     return false;
 }
 
-#endif
+template <bool FULL, bool CULL = false, bool FLAT = RT_OCCL_FLAT>
+__device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int li, uint64_t mask = ~0ull,
+                                         int skip = -1) {
+    if constexpr (FLAT) return occluded_flag<FULL, CULL>(V, r, li, mask, skip);
+    else return occluded_ret<FULL, CULL>(V, r, li, mask, skip);
+}
 
 // Material of a hit (checker parity for the board, :1101-1111).
 // (int)(x / square) for the checker, both quotients sharing one reciprocal r = rcp_core(square) (the
@@ -1432,7 +1438,9 @@ __device__ __forceinline__ d3 shade(const SceneView& V, bool hit, d3 p, d3 n, in
             if (in) m = in[t + lslot + i];
         }
         bool lit = false;
-        if (hit) lit = !(FULL ? occluded_transparent(V, sr) : occluded<false, CULL>(V, sr, i, m, skip));
+        if (hit)
+            lit = !(FULL ? occluded_transparent(V, sr)
+                         : occluded<false, CULL, RT_OCCL_FLAT && (ACHRO || !CULL)>(V, sr, i, m, skip));
         if (lit && ACHRO) {                                 // R only (same operations as below, channel x)
             const double a = S->att / (S->att + dl * dl);   // attenuation (:1181)
             const double lc = a * S->light[i].col[0];       // :1223
