@@ -36,12 +36,15 @@
 
 #include "rt_layout.hpp"
 
+// 1 (r06): the exact sqrt / quotient fast paths run unconditionally and their rare slow paths sit behind one
+// wave-uniform ballot branch (sqrt_fast, div_const, unit) instead of an exec-mask region per call site — fewer
+// scalar-stream instructions (in-process A/B c2 -4.5%, c3 -3.9%, c5 -5.5%, profiles/r06/ab; r02 measured +-0.8%).
+#ifndef RT_FAST_FALLBACK
+#define RT_FAST_FALLBACK 1
+#endif
 // 1: the exact tests of a filter batch visit its spheres in a loop the whole wave runs (record index
 // wave-uniform: scalar loads, SGPR operands; lanes whose filter rejected a sphere are masked off);
 // 0: each lane walks its own surviving spheres (per-lane index: vector loads).
-#ifndef RT_FAST_FALLBACK
-#define RT_FAST_FALLBACK 0
-#endif
 #ifndef RT_UNIFORM_PRIMARY
 #define RT_UNIFORM_PRIMARY 1
 #endif
