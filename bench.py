@@ -1202,16 +1202,18 @@ def main() -> int:
         la = [(ts[i % nf]._ctx, ctypes.byref(views[i % 16]), W, H, B, None,
                ctypes.c_void_p(bb[i % nf]["rgba32f"].data_ptr()), ctypes.c_void_p(bb[i % nf]["rgba8"].data_ptr()),
                None, None, ctypes.c_void_p(ss[i % nf].cuda_stream)) for i in range(nla)]
-        k = 96
-        wall, _ = pipelined_frames(torch, L, abi, ts, ss, la, k, min(args.settle, 0.1))
-        wall /= k
+        k = 96                                             # median of three passes (the clocks settled first)
+        walls = [pipelined_frames(torch, L, abi, ts, ss, la, k, min(args.settle, 0.3) if p == 0 else 0.0)[0] / k
+                 for p in range(3)]
+        wall = sorted(walls)[1]
         di["moving_camera"] = {"ms_per_frame": round(wall * 1e3, 4),
                                "value": round(sum(mrays) / 16 / wall / 1e6, 3),
                                "unit": "Mray/s", "static_view_ms_per_frame": round(ms_step, 4),
                                "frames_in_flight": nf,
+                               "passes_ms_per_frame": [round(w * 1e3, 4) for w in walls],
                                "note": "c2 scene, eye moves on a 16-view orbit, every frame a new eye "
                                        "(rt_prepare_kernel each frame; the tile-row order of the last calibrated "
-                                       "camera, re-timed every 8th frame)"}
+                                       "camera, re-timed every 8th frame); median of three passes of 96 frames"}
         for tt in ts[1:]:
             tt.close()
         t.close()

@@ -23,7 +23,8 @@ from ray_tracer_fragment_shader_amd.tracer import Tracer  # noqa: E402
 # mode:blocks[:split[:chunks]] — RT_SDMA_SPLIT (engines an SDMA frame copy is split over); RT_SDMA_CHUNKS (row chunks
 # of a synchronous SDMA frame) was an r05 experiment, no longer read; writer = RT_SDMA_WRITER (how the render stream
 # starts the SDMA copy: 1 stream write-value, 2 signal kernel, 0 the library's choice)
-SETTINGS = [tuple((x + ":2:2:2:0").split(":")[:5]) for x in
+_DEFAULTS = ["1", "0", "2", "2", "0"]                      # (mode, blocks, split, chunks, writer)
+SETTINGS = [tuple(x.split(":") + _DEFAULTS[len(x.split(":")):]) for x in
             os.environ.get("SETTINGS", "1:0,0:0,0:64,0:16,1:64,2:0").split(",")]
 # (RT_COPY_KERNEL=0 in the environment: hipMemcpyAsync — the runtime's blit kernel — instead of the copy kernel)
 L = abi.lib()
