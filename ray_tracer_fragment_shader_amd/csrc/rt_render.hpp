@@ -126,6 +126,9 @@ __host__ __device__ __forceinline__ int tile_col(int bx, int gy, int tiles_x) {
 // Slot of dispatch position L (linear workgroup id) in the dispatch table of n positions: grouped by L mod 8, the XCD
 // the round-robin dispatcher sends workgroup L to (up to a per-launch rotation), so each XCD reads a contiguous run
 // of the table and no L2 line is fetched by more than one XCD.
+#ifndef RT_DISP32
+#define RT_DISP32 0
+#endif
 __host__ __device__ __forceinline__ size_t cone_slot(size_t L, size_t n) { return (L & 7) * ((n + 7) >> 3) + (L >> 3); }
 __host__ __device__ __forceinline__ size_t cone_slots(size_t n) { return ((n + 7) >> 3) << 3; }
 
@@ -358,8 +361,16 @@ __device__ __forceinline__ void render_body(const DevScene* __restrict__ gscene,
     int tx = tile_col(bxd, gy, P.tiles_x), ty_raw = gy;
     uint64_t cone_cached = 0;
     if (disp) {
+#if RT_DISP32
+        // (32-bit index arithmetic: a frame's dispatch positions number < 2^31; cone_slot's value, fewer scalar ops
+        // on the chain to the wave's first dependent load)
+        const uint32_t n = (uint32_t)geom.n, Lp = (uint32_t)gy * (uint32_t)geom.tiles_x + (uint32_t)bxd;
+        const uint32_t Lc = Lp < n ? Lp : n - 1;
+        const DispRec rec = disp[(Lc & 7u) * ((n + 7u) >> 3) + (Lc >> 3)];   // (padding positions: in bounds, unused)
+#else
         const size_t n = (size_t)geom.n, Lp = (size_t)gy * geom.tiles_x + bxd;
         const DispRec rec = disp[cone_slot(Lp < n ? Lp : n - 1, n)];   // (padding positions: in bounds, unused)
+#endif
         asm volatile("" ::"s"(rec.cone_lo), "s"(rec.cone_hi), "s"(rec.tile));
         cone_cached = (uint64_t)rec.cone_lo | ((uint64_t)rec.cone_hi << 32);
         tx = (int)(rec.tile & 0xffffu);
