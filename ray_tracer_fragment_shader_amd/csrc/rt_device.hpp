@@ -1300,6 +1300,12 @@ __device__ __forceinline__ bool occluded(const SceneView& V, const Ray& r, int l
 // compiler's own Newton steps): for |x| in [2^-969, 2^500] and a normal `square` div_core is the IEEE
 // quotient bit for bit (fast paths above); below that the quotient is < 2^-400 and truncates to 0 either
 // way, hit points on the board never exceed it, and NaN stays NaN (converted to 0 either way).
+// MESH = false: the caller's closest hits never name a mesh triangle (the opaque kernels' closest_hit<false> tests no
+// meshes), so that branch is compiled out (RT_MESH_STATIC).
+#ifndef RT_MESH_STATIC
+#define RT_MESH_STATIC 1
+#endif
+template <bool MESH = true>
 __device__ __forceinline__ int material_of(const SceneView& V, int kind, d3 p) {
     const DevScene* S = V.S;
     if (kind == 0) {
@@ -1308,7 +1314,7 @@ __device__ __forceinline__ int material_of(const SceneView& V, int kind, d3 p) {
         int squareSum = (int)div_core(q.x, S->square, r) + (int)div_core(q.z, S->square, r);
         return (squareSum & 1) == 0 ? 0 : 1;
     }
-    if (kind >= kMeshKind) return V.mesh[(kind - kMeshKind) >> 4].mat;
+    if (MESH && kind >= kMeshKind) return V.mesh[(kind - kMeshKind) >> 4].mat;
     return 2;
 }
 
@@ -1338,11 +1344,12 @@ __device__ __forceinline__ d3 transmitted_end(const SceneView& V, int kind, int 
 #ifndef RT_CENTER_UNIFORM
 #define RT_CENTER_UNIFORM 0
 #endif
+template <bool MESH = true>
 __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u, d3* n, int* mat, d3* pe) {
     const DevScene* S = V.S;
     if (kind == 0) {
         *n = ld3(S->tri[0].n);
-    } else if (kind >= kMeshKind) {
+    } else if (MESH && kind >= kMeshKind) {
         const DevMesh& M = V.mesh[(kind - kMeshKind) >> 4];
         *n = ld3(V.tri[M.tri0 + ((kind - kMeshKind) & 15)].n);
     } else {
@@ -1366,7 +1373,7 @@ __device__ __forceinline__ void surface(const SceneView& V, int kind, d3 p, d3 u
         d3 dp = sub(p, c);                                  // directionP0 (:763)
         *n = unit(dp);                                      // :774-775
     }
-    *mat = material_of(V, kind, p);
+    *mat = material_of<MESH>(V, kind, p);
     d3 r = sub(u, scl(2 * dot(u, *n), *n));                 // :682 / :777
     *pe = add(p, r);                                        // Line(p, p + r)
 }
@@ -1606,7 +1613,7 @@ __device__ __forceinline__ bool cull_level(const SceneView& V, int lvl, bool fir
     double* psl = slot + 3 * lvl * SS;                      // this level's colour slot, written after shade
     if (hit) {
         d3 pe;
-        surface(V, kind, p, r->u, &n, &mat, &pe);
+        surface<TRANSP || !RT_MESH_STATIC>(V, kind, p, r->u, &n, &mat, &pe);
         const d3 rd = sub(pe, p);                           // reflectedRay = Line(p, p + r)
         const d3 rdir = unit(rd);                           // reflectedRay.direction()
         ks = fabs(dot(r->u, rdir));                         // |u . reflectedRay.direction()|
@@ -1707,7 +1714,7 @@ __device__ __forceinline__ d3 trace(const SceneView& V, d3 p0, d3 p1, uint64_t c
             if (hit) {
                 d3 n, pe;
                 int mat;
-                surface(V, kind, p, r.u, &n, &mat, &pe);
+                surface<TRANSP || !RT_MESH_STATIC>(V, kind, p, r.u, &n, &mat, &pe);
                 const d3 rd = sub(pe, p);                   // reflectedRay = Line(p, p + r)
                 const d3 rdir = unit(rd);                   // reflectedRay.direction()
                 const double ks = fabs(dot(r.u, rdir));     // |u . reflectedRay.direction()|
