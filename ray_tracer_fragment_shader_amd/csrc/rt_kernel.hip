@@ -572,7 +572,7 @@ struct rt_ctx {
     bool sd_pending[kSlots] = {};
     int sd_copies[kSlots] = {};                         // engine copies queued for slot b (1 or 2)
     int sd_writer = 0;                                  // sdma_fire: 1 stream write-value, 2 signal kernel
-    int sd_writer_req = 0;                              // RT_SDMA_WRITER (A/B): 1 or 2 forces the writer, 0 tries 1 then 2
+    int sd_writer_req = 0;                              // RT_SDMA_WRITER (A/B): 1 or 2 forces the writer, 0 tries 2 then 1
     int sd_wait_ms = 5000;                              // RT_SDMA_WAIT_MS: how often sdma_wait re-checks a slow render
     int last_copy_mode = -1;                            // the mode the last packed frame took (rt_diag_copy_path)
     uint64_t ticket = 0;                       // rt_render_packed_async frames queued so far
@@ -1310,11 +1310,14 @@ static bool sdma_init(rt_ctx* c) {
              hsa_signal_create(0, 0, nullptr, &c->sd_done[k][1]) == HSA_STATUS_SUCCESS &&
              hsa_amd_signal_value_pointer(c->sd_dep[k], &c->sd_dep_ptr[k]) == HSA_STATUS_SUCCESS &&
              hipEventCreateWithFlags(&c->sd_fired[k], hipEventDisableTiming) == hipSuccess;
-    // how the render stream fires it: the stream's own write (hipStreamWriteValue64), else a one-wave kernel's
-    // system-scope store; each is tried once on slot 0's signal and must be seen from the host
+    // how the render stream fires it: a one-wave kernel's system-scope store, else the stream's own write
+    // (hipStreamWriteValue64); each is tried once on slot 0's signal and must be seen from the host.  (r06: the kernel
+    // first — the same speed, profiles/r06/ab/copy_ab_sdma_writer.json — and a plain store into memory the HSA runtime
+    // allocated, where the write-value hands the runtime a pointer it did not allocate.)
     if (ok) {
         c->sd_writer = 0;
-        for (int w = 1; w <= 2 && !c->sd_writer; ++w) {
+        for (int w : {2, 1}) {
+            if (c->sd_writer) break;
             if (c->sd_writer_req && w != c->sd_writer_req) continue;
             hsa_signal_store_screlease(c->sd_dep[0], 1);
             if (sdma_fire(c, 0, w) == hipSuccess && hipStreamSynchronize(c->rs) == hipSuccess &&

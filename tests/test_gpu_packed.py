@@ -314,7 +314,7 @@ def test_render_packed_host_sync_and_async(tr, monkeypatch, copy_mode):
                 got = np.ctypeslib.as_array(ctypes.cast(pins[(f - 1) % 2], ctypes.POINTER(ctypes.c_uint8)), (H, W))
                 assert np.array_equal(got, want[(f - 1) % 2][..., 0]), f - 1
         assert tickets == sorted(tickets) and len(set(tickets)) == 8
-        assert _copy_path(t) == (_ASYNC_MODE[copy_mode], 1 if _ASYNC_MODE[copy_mode] == 3 else _copy_path(t)[1])
+        assert _copy_path(t) == (_ASYNC_MODE[copy_mode], 2 if _ASYNC_MODE[copy_mode] == 3 else _copy_path(t)[1])
         abi.check(L.rt_ctx_wait(t._ctx, 0), "rt_ctx_wait")
         assert L.rt_ctx_wait(t._ctx, tickets[-1] + 5) == abi.RT_EINVAL
     finally:

@@ -31,7 +31,8 @@ LIB=ray_tracer_fragment_shader_amd/lib/librt_amd.so
 if want tests; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} \
       > "$OUT/gpu_tests.log" 2>&1
-  rc=$?; tail -5 "$OUT/gpu_tests.log"; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit $rc; }
+  rc=$?; cp "$OUT/gpu_tests.log" "$OUT/gpu_tests_$(date +%H%M%S).log"; tail -5 "$OUT/gpu_tests.log"
+  [ $rc -eq 0 ] || { grep -n -i -A3 "memory access fault\|captured stderr" "$OUT/gpu_tests.log" | head -40; echo "pytest rc=$rc"; exit $rc; }
 fi
 if want smoke; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
