@@ -489,9 +489,9 @@ struct rt_ctx {
     // depth, outputs) view uses the identity order; the second render of the same view is a calibration
     // render that also times its tile rows; later renders dispatch the rows by decreasing time.  A render
     // of another camera with the same frame shape (size, rows, depth, outputs, scene) reuses the last
-    // calibrated order — row costs change slowly with the camera — and every kRecalibrate-th such render
-    // re-times the rows under it, so a moving camera keeps a longest-first order without paying for a
-    // calibration every frame.  Any order is a permutation of the tile rows: images never depend on it.
+    // calibrated order and every kRecalibrate-th such render re-times the rows under it when RT_MOVING_ORDER=1; by
+    // default (r06) it renders in identity order (moving_order below).  Any order is a permutation of the tile rows:
+    // images never depend on it.
     // order_mode (rt_diag_tile_order): 0 adaptive, 1 bottom-to-top.
     int32_t* d_tile_rows = nullptr;            // row order: tile rows by decreasing calibrated time
     uint32_t* d_row_cost = nullptr;            // ... their times (rt_rowsum_kernel)
@@ -514,6 +514,12 @@ struct rt_ctx {
     bool seen_valid = false;                   // `seen_key`: the last view rendered once in identity order
     ViewKey seen_key{};
     int stale = 0;                             // renders of other cameras since the order was calibrated
+    // r06: a moving camera renders in identity order (RT_MOVING_ORDER=1: the last calibrated order, re-timed every
+    // RT_RECALIBRATE-th render, 8 by default then — the r03-r05 policy).  tools/moving_probe.py, c2 orbit, 3 frames in
+    // flight: identity 22.8 us per frame, the static view's order kept 24.2, re-timed every 8th render 26.9 (the
+    // re-timing's order kernels stall the context's stream; the static view's row costs are not the orbit's).
+    int moving_order = 0;
+    int recalibrate = kRecalibrate;
     int order_mode = 0;
     // Primary cone masks of the calibrated view (scenes with >= kPrimaryConeMin spheres): the calibration render
     // writes each tile's mask (d_cone_tile), rt_disp_kernel puts them in the dispatch table, and later renders of
@@ -718,6 +724,8 @@ extern "C" int rt_ctx_create(int device, rt_ctx** out) {
     if (const char* e = getenv("RT_SDMA_SPLIT")) c->sd_split = std::min(std::max(atoi(e), 1), 2);
     if (const char* e = getenv("RT_SDMA_WRITER")) c->sd_writer_req = std::min(std::max(atoi(e), 0), 2);
     if (const char* e = getenv("RT_SDMA_WAIT_MS")) c->sd_wait_ms = std::max(atoi(e), 0);
+    if (const char* e = getenv("RT_MOVING_ORDER")) c->moving_order = atoi(e) != 0;
+    if (const char* e = getenv("RT_RECALIBRATE")) c->recalibrate = std::max(atoi(e), 0);
     if (const char* e = getenv("RT_COPY_BLOCKS")) c->copy_blocks = std::max(atoi(e), 0);
     if (const char* e = getenv("RT_COPY_KERNEL")) c->copy_kernel = std::min(std::max(atoi(e), -1), 1);
     if (const char* e = getenv("RT_CONE_CACHE")) c->cone_cache = atoi(e) != 0;
@@ -931,13 +939,15 @@ static int render_dev_impl(rt_ctx* c, const rt_camera* cam, int W, int H, int de
                 P.lmask_in = c->d_lmask;
                 P.lmask_stride = lm_stride;
             }
-        } else if (same_shape) {
+        } else if (same_shape && c->moving_order) {
             P.disp = c->d_disp;                         // another camera: the last calibrated order, its own masks
-            if (++c->stale >= kRecalibrate) {           // ... re-timed every kRecalibrate-th render
+            if (c->recalibrate > 0 && ++c->stale >= c->recalibrate) {   // ... re-timed every recalibrate-th render
                 calibrate = true;
                 c->order_valid = false;
             }
-        } else if (c->seen_valid && key == c->seen_key) {
+        } else if (c->seen_valid && key == c->seen_key) {   // (by default a moving camera's views come here: the
+                                                            // first render of a view in identity order, its second
+                                                            // the calibration — a camera that stops is calibrated)
             calibrate = true;                           // calibration render (identity order)
             c->order_valid = false;                     // rt_disp_kernel rewrites d_disp below
             // the calibration records one mask per tile from lane 0 of its wave: one-wave workgroups only

@@ -69,9 +69,9 @@ def test_tile_order_policy_frames_hash_to_the_reference(monkeypatch, name):
 
 
 def test_other_cameras_and_back(tr):
-    """A cached view, then cameras of the same frame shape (their own masks, the calibrated order reused and
-    re-timed every 8th render), then the cached view again: each frame equals a fresh context's first render
-    of that camera, and the cached view still hashes to the reference."""
+    """A cached view, then cameras of the same frame shape (their own masks; identity order by default, the
+    calibrated order reused and re-timed every 8th render with RT_MOVING_ORDER=1), then the cached view again: each
+    frame equals a fresh context's first render of that camera, and the cached view still hashes to the reference."""
     cfg = scenes.CONFIGS["c2"]
     W, H = cfg.width, cfg.height
     sc = cfg.scene()

@@ -450,21 +450,33 @@ def test_graph_replay_after_other_views(tr):
         assert np.array_equal(bufs["rgb64f"].cpu().numpy(), want), f"replay {k}"
 
 
-def test_moving_camera_reuses_order_exactly(tr):
-    """A camera that moves every frame: renders reuse the last calibrated tile-row order of the same frame
-    shape and re-time it every 8th frame (rt_ctx stale-order policy); every frame stays the oracle's, and
-    so does a size change in the middle (a new shape: identity order, then calibration)."""
+@pytest.mark.parametrize("policy", ["identity", "stale_order"])
+def test_moving_camera_reuses_order_exactly(tr, monkeypatch, policy):
+    """A camera that moves every frame, with a calibrated view of the same frame shape before it: by default (r06)
+    each new view renders in identity order (and a view rendered twice is calibrated); with RT_MOVING_ORDER=1 the
+    renders reuse the last calibrated tile-row order and re-time it every 8th frame (RT_RECALIBRATE, the r03-r05
+    policy).  Every frame stays the oracle's, and so does a size change in the middle (a new shape: identity order,
+    then calibration)."""
+    if policy == "stale_order":
+        monkeypatch.setenv("RT_MOVING_ORDER", "1")
+        monkeypatch.setenv("RT_RECALIBRATE", "8")
+    t = Tracer(0)
     cfg = scenes.CONFIGS["c2"]
     sc = cfg.scene()
-    tr.set_scene(sc)
+    t.set_scene(sc)
     sa = sc.to_abi()
-    for (W, H) in ((320, 180), (256, 200)):
-        for v in range(20):
-            cam = cfg.camera(W, H)
-            ang = 2.0 * np.pi * v / 20
-            cam.eye = abi.vec3((60.0 * np.sin(ang), 100.0 + 10.0 * np.cos(ang), 200.0))
-            b = tr.render(cam, W, H, cfg.depth, rgba32f=False, rgb64f=True, raycount=True)
-            torch.cuda.synchronize()
-            want, want_rc = po.render(sa, cam, W, H, cfg.depth)
-            assert np.array_equal(b["rgb64f"].cpu().numpy(), want), (W, v)
-            assert np.array_equal(b["raycount"].cpu().numpy().view(np.uint32), want_rc), (W, v)
+    try:
+        for (W, H) in ((320, 180), (256, 200)):
+            for _ in range(3):                          # the static view first: calibrated
+                t.render(cfg.camera(W, H), W, H, cfg.depth, rgba32f=False, rgb64f=True)
+            for v in range(20):
+                cam = cfg.camera(W, H)
+                ang = 2.0 * np.pi * v / 20
+                cam.eye = abi.vec3((60.0 * np.sin(ang), 100.0 + 10.0 * np.cos(ang), 200.0))
+                b = t.render(cam, W, H, cfg.depth, rgba32f=False, rgb64f=True, raycount=True)
+                torch.cuda.synchronize()
+                want, want_rc = po.render(sa, cam, W, H, cfg.depth)
+                assert np.array_equal(b["rgb64f"].cpu().numpy(), want), (W, v)
+                assert np.array_equal(b["raycount"].cpu().numpy().view(np.uint32), want_rc), (W, v)
+    finally:
+        t.close()

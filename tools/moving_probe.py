@@ -43,7 +43,7 @@ def run(case, ts, ss, views, bufs, L, W, H, B, k=96):
 
 def main():
     L = abi.lib()
-    cfg = scenes.CONFIGS["c2"]
+    cfg = scenes.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"]
     W, H, B = cfg.width, cfg.height, cfg.depth
     views = []
     for v in range(16):
@@ -61,6 +61,46 @@ def main():
     keep = [torch.cuda.Stream() for _ in range(24)]
     run("after_24_streams", ts, [torch.cuda.Stream() for _ in range(3)], views, bufs, L, W, H, B)
     run("one_stream_serial", ts[:1], [torch.cuda.Stream()], views, bufs, L, W, H, B)
+    # the bench's first context has rendered the static view (calibrated: its tile-row order is the static view's)
+    cam = cfg.camera()
+    st = torch.cuda.Stream()
+    for t in ts[:1]:
+        for _ in range(4):
+            abi.check(L.rt_render_dev(t._ctx, ctypes.byref(cam), W, H, B, None, ctypes.c_void_p(bufs[0][0].data_ptr()),
+                                      ctypes.c_void_p(bufs[0][1].data_ptr()), None, None,
+                                      ctypes.c_void_p(st.cuda_stream)), "rt_render_dev")
+    torch.cuda.synchronize()
+    run("first_ctx_calibrated_static", ts, [torch.cuda.Stream() for _ in range(3)], views, bufs, L, W, H, B)
+    for t in ts:
+        for _ in range(4):
+            abi.check(L.rt_render_dev(t._ctx, ctypes.byref(cam), W, H, B, None, ctypes.c_void_p(bufs[0][0].data_ptr()),
+                                      ctypes.c_void_p(bufs[0][1].data_ptr()), None, None,
+                                      ctypes.c_void_p(st.cuda_stream)), "rt_render_dev")
+    torch.cuda.synchronize()
+    run("all_ctx_calibrated_static", ts, [torch.cuda.Stream() for _ in range(3)], views, bufs, L, W, H, B)
+    fresh = [Tracer(0) for _ in range(3)]
+    for t in fresh:
+        t.set_scene(cfg.scene())
+    run("fresh_again", fresh, [torch.cuda.Stream() for _ in range(3)], views, bufs, L, W, H, B)
+    for t in fresh:
+        t.close()
+    # the same with the moving camera's re-timing off (RT_RECALIBRATE=0: the static view's order is kept) and at 32
+    for rc in ("default", "0", "8"):                       # default: identity order; else RT_MOVING_ORDER=1
+        if rc != "default":
+            os.environ["RT_MOVING_ORDER"], os.environ["RT_RECALIBRATE"] = "1", rc
+        cal = [Tracer(0) for _ in range(3)]
+        for t in cal:
+            t.set_scene(cfg.scene())
+            for _ in range(4):
+                abi.check(L.rt_render_dev(t._ctx, ctypes.byref(cam), W, H, B, None,
+                                          ctypes.c_void_p(bufs[0][0].data_ptr()), ctypes.c_void_p(bufs[0][1].data_ptr()),
+                                          None, None, ctypes.c_void_p(st.cuda_stream)), "rt_render_dev")
+        torch.cuda.synchronize()
+        run(f"all_calibrated_recalibrate_{rc}", cal, [torch.cuda.Stream() for _ in range(3)], views, bufs, L, W, H, B)
+        for t in cal:
+            t.close()
+    os.environ.pop("RT_RECALIBRATE", None)
+    os.environ.pop("RT_MOVING_ORDER", None)
     del keep
     for t in ts:
         t.close()
