@@ -267,10 +267,9 @@ _STREAM_POOL = []
 
 
 def frame_streams(torch, dev, stream, n):
-    """The bench's stream and n - 1 more for frames in flight, the same streams for every leg: HIP gives each new stream
-    a hardware queue when it is created (four per process here), so streams created late in the run — after the c4
-    legs' — can share a queue and serialise frames meant to overlap (the moving-camera leg: 28.3 against 23.5 us per
-    frame in a fresh process, tools/moving_probe.py)."""
+    """The bench's stream and n - 1 more for frames in flight, the same streams for every leg (created together at
+    start-up: HIP gives each new stream one of four hardware queues in creation order, and streams created later can
+    share the bench stream's queue and serialise frames meant to overlap)."""
     while len(_STREAM_POOL) < n - 1:
         _STREAM_POOL.append(torch.cuda.Stream(dev))
     return [stream] + _STREAM_POOL[:n - 1]
@@ -719,6 +718,10 @@ def main() -> int:
     # part 3, BENCH_r05).  This process's current stream becomes one, so torch work stays ordered with it.
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
+    # the frames-in-flight streams, created right after the bench's stream and before any context creates its own:
+    # HIP hands out its four hardware queues in creation order, so streams created together get distinct queues
+    # (created later, one shared the bench stream's queue: the moving-camera leg ran 28.2 against 23.0 us per frame)
+    frame_streams(torch, dev, stream, max(1, args.frames_in_flight))
 
     def barrier():
         if world > 1:
@@ -1195,8 +1198,8 @@ def main() -> int:
                                 "skipped (unchanged); includes launch, kernel, PCIe copy and synchronisation")
         di.update(packed_host_legs(t, sa, cam, W, H, B))
         di["dropin_binding"] = dropin_binding_legs(W, H, B, cfg)
-        # moving camera: a new eye every frame (per-eye preparation every frame; the tile-row order of the
-        # last calibrated camera, re-timed every 8th frame), frames in flight as in the static leg
+        # moving camera: a new eye every frame (per-eye preparation every frame; each new view in identity tile
+        # order), frames in flight as in the static leg
         views = []
         for v in range(16):
             c2 = cfg.camera()
@@ -1209,24 +1212,30 @@ def main() -> int:
         ts = [t] + [Tracer(local) for _ in range(nf - 1)]
         for tt in ts[1:]:
             tt.set_scene(scene)
-        ss = frame_streams(torch, dev, stream, nf)
+        # (streams of their own: on the streams that had run the static legs' frames the same moving frames measured
+        # 28.2 against 23.0 us per frame — cause not found; in a fresh process either kind measures 23 us,
+        # tools/moving_probe.py)
+        ss = [torch.cuda.Stream(dev) for _ in range(nf)]
         bb = [tt.alloc(W, H, rgba32f=True, rgba8=True) for tt in ts]
         nla = 16 * nf                                      # frame i: view i % 16 on stream i % nf
         la = [(ts[i % nf]._ctx, ctypes.byref(views[i % 16]), W, H, B, None,
                ctypes.c_void_p(bb[i % nf]["rgba32f"].data_ptr()), ctypes.c_void_p(bb[i % nf]["rgba8"].data_ptr()),
                None, None, ctypes.c_void_p(ss[i % nf].cuda_stream)) for i in range(nla)]
         k = 96                                             # median of three passes (the clocks settled first)
-        walls = [pipelined_frames(torch, L, abi, ts, ss, la, k, min(args.settle, 0.3) if p == 0 else 0.0)[0] / k
-                 for p in range(3)]
+        passes = [pipelined_frames(torch, L, abi, ts, ss, la, k, min(args.settle, 0.3) if p == 0 else 0.0)
+                  for p in range(3)]
+        walls = [w / k for w, _ in passes]
         wall = sorted(walls)[1]
         di["moving_camera"] = {"ms_per_frame": round(wall * 1e3, 4),
                                "value": round(sum(mrays) / 16 / wall / 1e6, 3),
                                "unit": "Mray/s", "static_view_ms_per_frame": round(ms_step, 4),
                                "frames_in_flight": nf,
                                "passes_ms_per_frame": [round(w * 1e3, 4) for w in walls],
+                               "interval_ms_in_flight": round(sorted(x for _, x in passes)[1], 4),
                                "note": "c2 scene, eye moves on a 16-view orbit, every frame a new eye "
-                                       "(rt_prepare_kernel each frame; the tile-row order of the last calibrated "
-                                       "camera, re-timed every 8th frame); median of three passes of 96 frames"}
+                                       "(rt_prepare_kernel each frame, primary cone masks in the kernel, each new "
+                                       "view in identity tile order — r06; RT_MOVING_ORDER=1 reuses the last "
+                                       "calibrated order); median of three passes of 96 frames"}
         for tt in ts[1:]:
             tt.close()
         t.close()
