@@ -7,6 +7,7 @@ The reference has one colour path (rayTraceRay, MySdlApplication.cpp:1184-1249);
 expands to the very bytes of the RGBA images a plain render writes — every test below checks that byte for byte,
 and the RGBA images themselves are pinned to the reference elsewhere (test_gpu_parity.py)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -514,15 +515,9 @@ def test_host_frames_into_pinned_interior_pointers(tr, offset):
         t.close()
 
 
-@pytest.mark.parametrize("writer", ["1", "2"])
-def test_render_packed_sdma_slow_render_is_not_a_failure(tr, monkeypatch, writer):
-    """sdma_wait's progress check at RT_SDMA_WAIT_MS=0 (every wait passes its deadline at once): a render still
-    running when the deadline passes is waited for, not released by hand, so no copy starts before its frame is in its
-    buffer — pipelined frames two behind, alternating views, each equal to the device render.  Both writers of the
-    render stream's dependency store (the stream's write-value operation and the signal kernel, RT_SDMA_WRITER)."""
-    monkeypatch.setenv("RT_COPY_MODE", "3")
-    monkeypatch.setenv("RT_SDMA_WAIT_MS", "0")
-    monkeypatch.setenv("RT_SDMA_WRITER", writer)
+def _slow_render_frames(tr, writer):
+    """The body of test_render_packed_sdma_slow_render_is_not_a_failure (RT_COPY_MODE=3, RT_SDMA_WAIT_MS=0 and
+    RT_SDMA_WRITER=writer already in the environment); also run as a child process for writer 1."""
     L = abi.lib()
     cfg = scenes.CONFIGS["c3"]
     sa = cfg.scene().to_abi()
@@ -558,3 +553,27 @@ def test_render_packed_sdma_slow_render_is_not_a_failure(tr, monkeypatch, writer
         for p in pins:
             L.rt_host_free(p)
         t.close()
+
+
+@pytest.mark.parametrize("writer", ["1", "2"])
+def test_render_packed_sdma_slow_render_is_not_a_failure(tr, monkeypatch, writer):
+    """sdma_wait's progress check at RT_SDMA_WAIT_MS=0 (every wait passes its deadline at once): a render still
+    running when the deadline passes is waited for, not released by hand, so no copy starts before its frame is in its
+    buffer — pipelined frames two behind, alternating views, each equal to the device render.  Both writers of the
+    render stream's dependency store (RT_SDMA_WRITER): the signal kernel (the default) here, the stream's write-value
+    operation in a child process of its own — it hands the HIP runtime a pointer into HSA signal memory, and this
+    process's later device-to-host copies are kept clear of whatever that leaves behind."""
+    monkeypatch.setenv("RT_COPY_MODE", "3")
+    monkeypatch.setenv("RT_SDMA_WAIT_MS", "0")
+    monkeypatch.setenv("RT_SDMA_WRITER", writer)
+    if writer == "2":
+        _slow_render_frames(tr, writer)
+        return
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); from tests import test_gpu_packed as m; "
+            "from ray_tracer_fragment_shader_amd.tracer import Tracer; t = Tracer(0); "
+            "m._slow_render_frames(t, %r); t.close(); print('ok')" % (root, writer))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
