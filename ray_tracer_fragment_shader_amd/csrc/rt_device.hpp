@@ -443,7 +443,13 @@ __device__ __forceinline__ bool board_hit(const DevScene* S, d3 p0, d3 d, d3* p)
     bool hit = false;
     if (live) {
         double m = num / nd;                                // :657
+#if RT_BOARD_FLAT >= 2
+        // (:659's m < eps folded into the decision below: one region less; the hit point of such a lane is unused)
+        const bool far_enough = !(m < S->eps);
+        {
+#else
         if (!(m < S->eps)) {                                // :659
+#endif
             d3 q = add(p0, scl(m, d));                      // :665
             d3 w = sub(q, v0);                              // :667
             bool decided = false;
@@ -456,6 +462,10 @@ __device__ __forceinline__ bool board_hit(const DevScene* S, d3 p0, d3 d, d3* p)
                 hit = in;
                 decided = in | outside;
             }
+#endif
+#if RT_BOARD_FLAT >= 2
+            hit &= far_enough;
+            decided |= !far_enough;
 #endif
             if (!decided) {
 #pragma unroll
