@@ -551,8 +551,11 @@ void rt_render_kernel_sg(const DispRec* __restrict__ disp, int32_t tiles_x, int3
 #ifndef RT_FAST8_SGPRS
 #define RT_FAST8_SGPRS 78
 #endif
+// r06: off (-1).  After the r06 scalar-stream cuts the plain depth-2 instance needs 94 SGPRs and 64 VGPRs — 8 waves per
+// SIMD with no spills — and measured c3 -0.9% serial, -3.1% in flight against the capped one
+// (profiles/r06/ab/ab_libs_nosg8*.jsonl).
 #ifndef RT_SG8_B
-#define RT_SG8_B 2
+#define RT_SG8_B -1
 #endif
 #ifndef RT_SG8_MINW
 #define RT_SG8_MINW 8                          // r06: the 8-wave kernel asks for 8 waves (<= 64 VGPRs) explicitly
