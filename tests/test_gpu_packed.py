@@ -322,6 +322,8 @@ def test_sdma_cases_in_child_process():
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and r.stdout.strip().endswith("done"), (r.returncode, r.stdout[-3000:], r.stderr[-3000:])
     assert r.stdout.count("ok ") + r.stdout.count("skipped ") == len(_SDMA_CASES), r.stdout
+    assert r.stdout.count("ok ") >= len(_SDMA_CASES) - 1, r.stdout      # (only the host-register case may skip)
+    print(r.stdout)
 
 
 @pytest.mark.parametrize("copy_mode", COPY_MODES, ids=["default", "copy_stream", "sdma"])
