@@ -551,8 +551,9 @@ void rt_render_kernel_sg(const DispRec* __restrict__ disp, int32_t tiles_x, int3
 #ifndef RT_FAST8_SGPRS
 #define RT_FAST8_SGPRS 78
 #endif
-// r06: off (-1).  After the r06 scalar-stream cuts the plain depth-2 instance needs 94 SGPRs and 64 VGPRs — 8 waves per
-// SIMD with no spills — and measured c3 -0.9% serial, -3.1% in flight against the capped one
+// r06: off (-1).  After the r06 scalar-stream cuts the plain depth-2 instance needs 94 SGPRs and 64 VGPRs with no
+// spills — 7 waves per SIMD on the hardware (8 need <= 78 SGPRs, above; the compiler reports 8) — and measured c3
+// -0.9% serial, -3.1% in flight against the capped 8-wave one with its 58 spilled SGPRs
 // (profiles/r06/ab/ab_libs_nosg8*.jsonl).
 #ifndef RT_SG8_B
 #define RT_SG8_B -1
